@@ -1,0 +1,288 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident RX parse + checksum + flow-hash on MI355X.
+
+A step = one pass of the hot path (one ixg_rx_batch_dev launch) over one
+batch of synthetic frames already resident in HBM. Default workload = the
+configuration BASELINE.json's metric is quoted on: configs[1], 16,777,216
+64-byte Eth/IPv4/TCP frames on one GPU. A 1514-byte shard (C4's per-GPU
+shape) is measured as the secondary line. N>1: one process per GPU, each
+with its own batch (weak scaling), no collective on the data path; the
+timed region is bracketed by barrier + synchronize and the max over ranks
+is taken.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mpkt/s + GB/s device-resident RX parse+cksum+flow-hash, 64B & 1500B frames"
+PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+WORKLOADS = {
+    # name: (trace kind, frames per GPU, distinct frames in the pool, description)
+    "c2": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2: 16M x 64B Eth/IPv4/TCP frames (L=60, stride 60), 1 GPU"),
+    "c4": ("tcp1514", 8 * 1024 * 1024, 1 << 13, "C4 per-GPU shard: 8M x 1514B IPv4/TCP frames (stride 1516)"),
+    "c3": ("imix", 16 * 1024 * 1024, 1 << 18, "C3: 16M IMIX 7:4:1 (60/590/1514B) TCP+UDP, packed, u64 offsets"),
+    "c5": ("mixed", 16 * 1024 * 1024, 1 << 18, "C5: 16M mixed IPv4 ihl 5..15 + 50% IPv6, packed"),
+}
+
+
+def alg_bytes(tr) -> np.ndarray:
+    """Algorithmic bytes read per frame: 14 + ip_len for
+    IPv4 (the Ethernet header plus the IP datagram; padding excluded), 54 +
+    payload for IPv6, plus the descriptor and the 16-byte record."""
+    offs = tr.offsets().astype(np.int64)
+    b = tr.blob
+    et = (b[offs + 12].astype(np.int64) << 8) | b[offs + 13]
+    v4 = (b[offs + 16].astype(np.int64) << 8) | b[offs + 17]
+    v6 = (b[offs + 18].astype(np.int64) << 8) | b[offs + 19]
+    rd = np.where(et == 0x86DD, 54 + v6, 14 + v4)
+    rd = np.minimum(rd, tr.len.astype(np.int64))
+    desc = 2 + (8 if tr.off is not None else 0)
+    return rd + desc + 16
+
+
+class Workload:
+    """A batch of n frames on `dev`, tiled from `pool` distinct frames."""
+
+    def __init__(self, name: str, seed: int, dev, n: int | None = None):
+        import torch
+        from ix_amd import traces
+        kind, n_def, pool, self.desc = WORKLOADS[name]
+        self.name = name
+        self.n = n or n_def
+        pool = min(pool, self.n)
+        assert self.n % pool == 0
+        self.reps = self.n // pool
+        self.pool = traces.make_trace(kind, pool, seed=seed)
+        self.flags = 2 if kind == "mixed" else 0
+        tr = self.pool
+        self.bytes_per_pkt = float(alg_bytes(tr).mean())
+        self.wire_bytes = float(tr.len.astype(np.int64).mean())
+        if tr.off is None:
+            S = tr.stride
+            self.stride = S
+            src = torch.from_numpy(tr.blob[:pool * S]).to(dev)
+            self.blob = torch.zeros(self.n * S + traces.TAIL_PAD, dtype=torch.uint8, device=dev)
+            self.blob[:self.n * S].view(self.reps, pool * S).copy_(src.unsqueeze(0).expand(self.reps, -1))
+            self.off = None
+        else:
+            self.stride = 0
+            span = int(tr.off[-1]) + ((int(tr.len[-1]) + 3) // 4) * 4
+            src = torch.from_numpy(tr.blob[:span]).to(dev)
+            self.blob = torch.zeros(self.reps * span + traces.TAIL_PAD, dtype=torch.uint8, device=dev)
+            self.blob[:self.reps * span].view(self.reps, span).copy_(src.unsqueeze(0).expand(self.reps, -1))
+            o = torch.from_numpy(tr.off.view(np.int64)).to(dev)
+            k = torch.arange(self.reps, device=dev, dtype=torch.int64).unsqueeze(1) * span
+            self.off = (o.unsqueeze(0) + k).reshape(-1).contiguous()
+        ln = torch.from_numpy(tr.len.view(np.int16)).to(dev)
+        self.len = ln.repeat(self.reps).contiguous()
+        self.out = torch.empty((self.n, 16), dtype=torch.uint8, device=dev)
+
+    def launch(self, eng, stream) -> None:
+        eng.batch_dev(self.blob.data_ptr(), None if self.off is None else self.off.data_ptr(),
+                      self.len.data_ptr(), self.stride, self.n, self.out.data_ptr(), None, stream)
+
+    def check(self, key: bytes) -> bool:
+        """Records of the tiled batch == the oracle's records of the pool, tiled."""
+        import torch
+        from oracle import oracle
+        er, _ = oracle.rx_trace(self.pool, key, flags=self.flags, threads=8, hash_mode=oracle.HASH_TABLE)
+        exp = torch.from_numpy(er).to(self.out.device)
+        return bool(torch.equal(self.out.view(self.reps, -1, 16), exp.unsqueeze(0).expand(self.reps, -1, -1)))
+
+
+def time_steps(wl, eng, steps, warmup, dist, world):
+    import torch
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    for _ in range(warmup):
+        wl.launch(eng, sp)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        wl.launch(eng, sp)
+        b.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    kern = [a.elapsed_time(b) * 1e-3 for a, b in ev]
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el, float(np.mean(kern)), float(np.min(kern))
+
+
+def cpu_baseline(tr, flags, key, seconds: float, threads: int):
+    """The oracle (C restatement, table-driven hashes) on host cores over a
+    bounded sample of the same workload (its pool of distinct frames)."""
+    from oracle import oracle
+    done, t0 = 0, time.perf_counter()
+    while True:
+        oracle.rx_trace(tr, key, flags=flags, threads=threads, hash_mode=oracle.HASH_TABLE)
+        done += tr.n
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return done / el / 1e6, done, el
+
+
+def copy_inclusive(wl, eng, key, reps=3):
+    """Host-resident batch: H2D frames (pinned) + kernel + D2H records."""
+    import torch
+    n = wl.n
+    h_blob = wl.blob.cpu().pin_memory()
+    h_len = wl.len.cpu().pin_memory()
+    h_off = None if wl.off is None else wl.off.cpu().pin_memory()
+    h_out = torch.empty((n, 16), dtype=torch.uint8).pin_memory()
+    s = torch.cuda.current_stream()
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wl.blob.copy_(h_blob, non_blocking=True)
+        wl.len.copy_(h_len, non_blocking=True)
+        if h_off is not None:
+            wl.off.copy_(h_off, non_blocking=True)
+        wl.launch(eng, s.cuda_stream)
+        h_out.copy_(wl.out, non_blocking=True)
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    h2d = h_blob.numel() + h_len.numel() * 2 + (0 if h_off is None else h_off.numel() * 8)
+    return {"mpps": n / best / 1e6, "seconds": best, "h2d_bytes": int(h2d), "d2h_bytes": int(n * 16),
+            "link_gbps": (h2d + n * 16) / best / 1e9}
+
+
+def load_traffic(workload: str):
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(p):
+        return None, None
+    d = json.load(open(p))
+    e = d.get(workload)
+    if not e:
+        return None, None
+    return e.get("hbm_bytes_per_launch"), e.get("source")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
+    ap.add_argument("--secondary", default="c4", help="second workload line ('' to skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-copy", action="store_true")
+    ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
+    args = ap.parse_args()
+
+    import torch
+    from ix_amd import ixgrx, traces
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+    key = traces.RSS_KEY
+    eng = ixgrx.RxEngine(ixgrx.Config(key, 128, rank % 128, 0), device=local)
+    eng2 = None
+
+    wl = Workload(args.workload, seed=0x1B0000 + 2 + 97 * rank, dev=dev, n=args.n)
+    el, kavg, kmin = time_steps(wl, eng, args.steps, args.warmup, dist, world)
+    ok = wl.check(key) if rank == 0 else True
+    primary = (wl.name, wl.pool, wl.flags)
+    total = wl.n * args.steps * world
+    mpps = total / el / 1e6
+    bpl = wl.bytes_per_pkt * wl.n  # algorithmic bytes per launch (one GPU)
+    achieved = bpl / kavg / 1e9
+    traffic, tsrc = load_traffic(args.workload)
+    res = {
+        "metric": METRIC,
+        "value": round(mpps, 2),
+        "unit": "Mpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": f"synthetic ({wl.pool.n} distinct frames tiled to {wl.n} per GPU, valid checksums)",
+        "config": {"workload": wl.desc, "frames_per_gpu": wl.n, "wire_bytes_per_frame": wl.wire_bytes,
+                   "layout": "fixed stride" if wl.off is None else "packed + u64 offsets",
+                   "parallelism": f"shard{world}"},
+        "gbps_algorithmic": round(mpps * wl.bytes_per_pkt / 1e3, 2),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
+                     "alg_bytes_per_pkt": round(wl.bytes_per_pkt, 2), "kernel_ms_avg": round(kavg * 1e3, 4),
+                     "kernel_ms_min": round(kmin * 1e3, 4), "kernel": "ixg_rx_kernel",
+                     "traffic_source": tsrc},
+        "parity": "ok" if ok else "MISMATCH",
+    }
+    if args.secondary and args.secondary != args.workload:
+        del wl
+        torch.cuda.empty_cache()
+        wl2 = Workload(args.secondary, seed=0x1B0000 + 4 + 97 * rank, dev=dev)
+        el2, k2, _ = time_steps(wl2, eng, max(5, args.steps // 2), 2, dist, world)
+        ok2 = wl2.check(key) if rank == 0 else True
+        m2 = wl2.n * max(5, args.steps // 2) * world / el2 / 1e6
+        a2 = wl2.bytes_per_pkt * wl2.n / k2 / 1e9
+        res["secondary"] = {"workload": wl2.desc, "mpps": round(m2, 2),
+                            "gbps_algorithmic": round(m2 * wl2.bytes_per_pkt / 1e3, 1),
+                            "roofline_frac": round(a2 / PEAK_HBM_GBPS, 4), "kernel_ms_avg": round(k2 * 1e3, 4),
+                            "alg_bytes_per_pkt": round(wl2.bytes_per_pkt, 1),
+                            "parity": "ok" if ok2 else "MISMATCH"}
+        wl = wl2
+    if rank == 0 and world == 1 and not args.no_copy:
+        del wl
+        torch.cuda.empty_cache()
+        wlc = Workload(args.workload, seed=0x1B0000 + 2, dev=dev, n=args.n)
+        res["copy_inclusive"] = copy_inclusive(wlc, eng, key)
+        del wlc
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = min(16, os.cpu_count() or 1)
+        pname, ptr, pflags = primary
+        v, done, secs = cpu_baseline(ptr, pflags, key, args.cpu_seconds, threads)
+        v1, done1, secs1 = cpu_baseline(ptr, pflags, key, max(2.0, args.cpu_seconds / 4), 1)
+        res["cpu_baseline"] = {"value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+                               "sample": f"oracle/ixgrx_oracle.c (table-driven hashes) over {done} frames "
+                                         f"of the {pname} pool in {secs:.1f}s",
+                               "value_1core": round(v1, 2)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+    if eng2:
+        eng2.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,205 @@
+/*
+ * ixgrx.h - C ABI of the MI355X-native RX parse + checksum + flow-hash engine.
+ *
+ * This is the drop-in boundary for IX's receive-side per-packet transform:
+ * the work that dp/net + dp/lwip do on every frame between the driver poll
+ * and the TCP state machine. IX has no plugin API for this path; the two
+ * seams it replaces are
+ *
+ *   1. the driver vtable  struct eth_rx_queue { poll, ready }
+ *        (/root/reference/inc/ix/ethqueue.h:47-64), whose ixgbe implementation
+ *        fills mbuf->len / mbuf->fg_id from the RX descriptor (RSS) and drops
+ *        packets on the NIC checksum verdict (dp/drivers/ixgbe.c:286-376);
+ *   2. the direct call  eth_input(struct eth_rx_queue *, struct mbuf *)
+ *        (inc/ix/mbuf.h:232-234, dp/net/ip.c:120-141) made per packet by
+ *        eth_process_recv_queue (dp/core/ethqueue.c:91-110), which runs
+ *        ip_input (dp/net/ip.c:63-114), the tcp_input head
+ *        (dp/lwip/misc.c:57-67, dp/net/tcp_in.c:157-241), udp_input
+ *        (dp/net/udp.c:53-89) and icmp_input (dp/net/icmp.c:78-115).
+ *
+ * One call turns a batch of frames into one 16-byte record per frame, in
+ * input order. No C++ or HIP types appear here: streams are passed as void*
+ * (a hipStream_t), device buffers as plain pointers.
+ *
+ * Threading follows IX's per-CPU model: one context per host thread; calls on
+ * one context are not thread-safe. The library never frees or modifies an
+ * input frame (the reference rewrites TCP header fields to host order in
+ * place, tcp_in.c:230-238, and UDP writes an ip_tuple over the frame start,
+ * udp.c:81-86; both are host-side consumers' business here).
+ */
+#ifndef IXGRX_H
+#define IXGRX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IXGRX_ABI_VERSION 1
+
+/* Constants of the reference this ABI is bit-exact against. */
+#define IXG_ETH_MAX_NUM_FG 512u    /* inc/ix/ethfg.h:38 ETH_MAX_NUM_FG */
+#define IXG_PCB_BUCKETS 512u       /* inc/ix/ethfg.h:42 TCP_ACTIVE_PCBS_MAX_BUCKETS */
+#define IXG_PCB_HASH_SEED 0xa36bdcbeu /* inc/lwip/lwip/tcp_impl.h:371 */
+#define IXG_MBUF_HEADER_LEN 64u    /* inc/ix/mbuf.h MBUF_HEADER_LEN: data at mbuf+64 */
+#define IXG_MBUF_DATA_LEN 2048u    /* inc/ix/mbuf.h MBUF_DATA_LEN */
+#define IXG_MBUF_STRIDE 2112u      /* MBUF_LEN, element stride of the mbuf mempool */
+#define IXG_RSS_KEY_LEN 40u
+
+/* Bytes that must be readable past the end of the last frame of a device
+ * batch (the kernels load 16-byte chunks and may run up to 15 bytes past L). */
+#define IXG_TAIL_PAD 64u
+
+/* ---- configuration -------------------------------------------------- */
+
+/* cfg.flags */
+#define IXG_F_NO_CSUM_DROP (1u << 0) /* report checksum flags but never turn a
+                                        bad checksum into a DROP verdict (IX
+                                        with hw_ip_checksum=0) */
+#define IXG_F_IPV6 (1u << 1)         /* extension: parse IPv6 TCP/UDP instead
+                                        of the reference's ethertype drop */
+
+struct ixg_rx_cfg {
+	uint8_t rss_key[IXG_RSS_KEY_LEN]; /* Toeplitz key; IX leaves the NIC/DPDK
+	                                     default (dp/drivers/common.c:136-168) */
+	uint16_t nb_rx_fgs; /* RETA size, power of two <= 512 (common.c:257) */
+	uint16_t dev_idx;   /* fg_id = dev_idx*512 + local fg (dp/core/init.c:456-462) */
+	uint32_t flags;     /* IXG_F_* */
+};
+
+/* ---- the record ------------------------------------------------------- */
+
+/* verdict: what IX's RX path does with the frame. Deliveries are < 0x80. */
+enum ixg_verdict {
+	IXG_V_TCP = 0x01,       /* -> tcp_input body (tcp_in.c:243-): l4_off/l4_len
+	                           = TCP payload after the doff strip (tcp_in.c:222),
+	                           pcb_bucket = tcp_to_idx (tcp_in.c:233) */
+	IXG_V_UDP = 0x02,       /* -> usys_udp_recv(data, len) (udp.c:88): l4_off =
+	                           UDP header + 8, l4_len = udp->len (header-inclusive,
+	                           as the reference reports it) */
+	IXG_V_ICMP_ECHO = 0x03, /* -> icmp_reflect (icmp.c:89-92): l4_off = ICMP
+	                           header, l4_len = ip_len - ihl*4 */
+	IXG_V_ARP = 0x04,       /* -> arp_input (ip.c:134-135): l4_off = 14,
+	                           l4_len = L - 14 */
+	IXG_V_TCP6 = 0x05,      /* IXG_F_IPV6 only: IPv6 TCP, fields as IXG_V_TCP */
+	IXG_V_UDP6 = 0x06,      /* IXG_F_IPV6 only: IPv6 UDP, fields as IXG_V_UDP */
+
+	/* drops: the caller frees the mbuf (ip.c:112-113,137) */
+	IXG_V_DROP_ETHERTYPE = 0x80,  /* ip.c:136-137 (IPv6, VLAN, other) */
+	IXG_V_DROP_IP_SHORT = 0x81,   /* ip.c:68  L < 14 + 20 */
+	IXG_V_DROP_IP_VERSION = 0x82, /* ip.c:71  version != 4 */
+	IXG_V_DROP_IP_IHL = 0x83,     /* ip.c:74  ihl < 5 */
+	IXG_V_DROP_IP_FRAG = 0x84,    /* ip.c:78  MF set or offset != 0 */
+	IXG_V_DROP_IP_LEN = 0x85,     /* ip.c:85  ip_len < ihl*4 */
+	IXG_V_DROP_IP_TRUNC = 0x86,   /* ip.c:87  14 + ip_len > L */
+	IXG_V_DROP_IP_PROTO = 0x87,   /* ip.c:106 proto not TCP/UDP/ICMP */
+	IXG_V_DROP_TCP_SHORT = 0x88,  /* tcp_in.c:189 l4len < 20 */
+	IXG_V_DROP_TCP_HDRLEN = 0x89, /* tcp_in.c:222 doff*4 > l4len */
+	IXG_V_DROP_UDP_LEN = 0x8a,    /* udp.c:59 udp->len past the frame */
+	IXG_V_DROP_ICMP_SHORT = 0x8b, /* icmp.c:80 len < 8 */
+	IXG_V_DROP_ICMP_CSUM = 0x8c,  /* icmp.c:82 chksum_internet != 0 */
+	IXG_V_DROP_ICMP_TYPE = 0x8d,  /* icmp.c:93-108 not an echo request */
+	IXG_V_DROP_CSUM_IP = 0x8e,    /* NIC IPCS&IPE (ixgbe.c:313-317) */
+	IXG_V_DROP_CSUM_L4 = 0x8f,    /* NIC L4CS&TCPE (ixgbe.c:320-324) */
+	IXG_V_DROP_IP6 = 0x90,        /* IXG_F_IPV6: malformed/unsupported IPv6 */
+};
+
+/* rec.flags */
+#define IXG_RF_IP_CSUM_CHECKED 0x01u
+#define IXG_RF_IP_CSUM_OK 0x02u
+#define IXG_RF_L4_CSUM_CHECKED 0x04u
+#define IXG_RF_L4_CSUM_OK 0x08u
+#define IXG_RF_RSS 0x10u /* rss_hash was computed (non-fragmented IPv4 TCP/UDP) */
+
+#define IXG_NO_BUCKET 0xffffu
+
+struct ixg_rx_rec {
+	uint16_t fg_id;      /* dev_idx*512 + (rss_hash & (nb_rx_fgs-1)) (ixgbe.c:329-335) */
+	uint8_t verdict;     /* enum ixg_verdict */
+	uint8_t flags;       /* IXG_RF_* */
+	uint16_t l4_off;     /* payload offset from the frame start (see verdicts) */
+	uint16_t l4_len;     /* payload length as the reference reports it */
+	uint32_t rss_hash;   /* raw Toeplitz hash (compute_toeplitz_hash, tcp_api.c:581-604); 0 if !IXG_RF_RSS */
+	uint16_t pcb_bucket; /* tcp_to_idx (tcp_impl.h:381-387) for IXG_V_TCP, else IXG_NO_BUCKET */
+	uint8_t tcp_flags;   /* TCPH_FLAGS (tcp_in.c:240) for IXG_V_TCP/TCP6, else 0 */
+	uint8_t rsvd;        /* 0 */
+};
+
+/* Optional per-frame checksum residuals (debug/parity): bits 0-15 =
+ * chksum_internet over the IP header, bits 16-31 = pseudo-header L4
+ * residual (inet_chksum_pseudo_partial). 0xffff in a half = not computed. */
+typedef uint32_t ixg_csum_t;
+
+/* ---- frames ------------------------------------------------------------ */
+
+/* A device-resident batch. Frame i starts at base + off[i] (or base +
+ * i*stride when off == NULL) and is len[i] bytes long (mbuf->len: CRC
+ * stripped, ethdev.c:50). Frame starts must be 4-byte aligned. Bytes at
+ * offsets >= len[i] are treated as zero. IXG_TAIL_PAD bytes past the last
+ * frame must be readable. */
+struct ixg_rx_frames {
+	const void *base;
+	const uint64_t *off; /* device array of n byte offsets, or NULL */
+	const uint16_t *len; /* device array of n frame lengths */
+	uint32_t stride;     /* used when off == NULL; multiple of 4 */
+	uint32_t rsvd;
+};
+
+/* ---- entry points ---------------------------------------------------- */
+
+/* Create a context on HIP device `device`. 0 or -errno. */
+int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **ctx);
+void ixg_rx_fini(void *ctx);
+
+/* Device-resident batch: records into device memory `d_out` (n entries),
+ * optional residuals into `d_csum` (n entries or NULL), enqueued on `stream`
+ * (a hipStream_t, NULL = default stream). Asynchronous. 0 or -errno. */
+int ixg_rx_batch_dev(void *ctx, const struct ixg_rx_frames *frames, uint32_t n,
+		     struct ixg_rx_rec *d_out, ixg_csum_t *d_csum, void *stream);
+
+/* Host batch in IX's own layout: n mbuf pointers (len = size_t at +0, frame
+ * data at +64, inc/ix/mbuf.h:73-90). Frames are gathered into pinned
+ * staging, copied to the device, processed, and the records copied back to
+ * host `out`. Synchronous. 0 or -errno. */
+int ixg_rx_batch_mbufs(void *ctx, void *const *mbufs, uint32_t n, struct ixg_rx_rec *out);
+
+/* Host batch from a packed host buffer (same layout rules as
+ * ixg_rx_frames, but host pointers). Synchronous. `csum` may be NULL. */
+int ixg_rx_batch_host(void *ctx, const void *frames, const uint64_t *off,
+		      const uint16_t *len, uint32_t stride, uint32_t n,
+		      struct ixg_rx_rec *out, ixg_csum_t *csum);
+
+/* The RSS/PCB hash tables the kernels use (12 x 256 x u64: low word =
+ * Toeplitz contribution, high word = CRC-32C contribution) and the CRC
+ * constant term, built from cfg on the host. For tests. */
+int ixg_rx_hash_tables(const struct ixg_rx_cfg *cfg, uint64_t *tab12x256, uint32_t *crc_const);
+
+int ixg_abi_version(void);
+const char *ixg_strerror(int err);
+
+/* ---- host-side dispatch: the eth_input replacement ------------------- */
+
+/* Callbacks a run-to-completion loop supplies; each receives the mbuf and
+ * its record. `drop` frees (mbuf_free). Mirrors the callees of eth_input /
+ * ip_input (ip.c:92-110,132-137) and of the tcp_input head. */
+struct ixg_rx_ops {
+	void (*tcp)(void *user, void *mbuf, const struct ixg_rx_rec *rec);
+	void (*udp)(void *user, void *mbuf, const struct ixg_rx_rec *rec);
+	void (*icmp_echo)(void *user, void *mbuf, const struct ixg_rx_rec *rec);
+	void (*arp)(void *user, void *mbuf, const struct ixg_rx_rec *rec);
+	void (*drop)(void *user, void *mbuf, const struct ixg_rx_rec *rec);
+};
+
+/* Dispatch n records in input order; returns the number delivered
+ * (non-drop). Replaces the per-packet eth_input loop of eth_process_recv
+ * (dp/core/ethqueue.c:117-149). */
+uint32_t ixg_rx_dispatch(void *const *mbufs, const struct ixg_rx_rec *recs, uint32_t n,
+			 const struct ixg_rx_ops *ops, void *user);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IXGRX_H */

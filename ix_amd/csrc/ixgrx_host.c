@@ -1,0 +1,429 @@
+/*
+ * ixgrx_host.c - the C host side of the RX engine: contexts, hash tables,
+ * device and host batch entry points, and the eth_input-replacing dispatch.
+ *
+ * Plain C over the HIP runtime API; the kernels live in ixgrx_kernels.hip.
+ * Semantics of every record field: include/ixgrx.h and DESIGN.md.
+ */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ixgrx.h"
+#include "ixgrx_internal.h"
+
+struct ixg_ctx {
+	int device;
+	struct ixg_rx_cfg cfg;
+	uint32_t crc_const;
+	uint32_t grid_max;
+	uint64_t *d_tab;
+	uint32_t *d_tab6;
+	hipStream_t stream; /* for the synchronous host paths */
+	/* host-path staging */
+	uint8_t *h_frames;
+	size_t h_frames_cap;
+	uint64_t *h_off;
+	uint16_t *h_len;
+	size_t h_n_cap;
+	uint8_t *d_frames;
+	size_t d_frames_cap;
+	uint64_t *d_off;
+	uint16_t *d_len;
+	struct ixg_rx_rec *d_out;
+	uint32_t *d_csum;
+	size_t d_n_cap;
+};
+
+/* ---- hash tables -------------------------------------------------------- */
+
+/* CRC-32C step as x86 crc32q (inc/ix/hash.h:35-39): reflected 0x82F63B78,
+ * no inversion, operand bytes least significant first */
+static uint32_t crc32c_u64(uint32_t crc, uint64_t v)
+{
+	for (int k = 0; k < 64; k++) {
+		crc ^= (uint32_t)(v >> k) & 1u;
+		crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+	}
+	return crc;
+}
+
+static uint32_t crc_stream(uint32_t seed, const uint8_t s[24])
+{
+	uint64_t w[3];
+	memcpy(w, s, 24);
+	return crc32c_u64(crc32c_u64(crc32c_u64(seed, w[0]), w[1]), w[2]);
+}
+
+/* Toeplitz contribution of byte value v at tuple position i: the 32-bit
+ * key windows starting at key bits 8i..8i+7, XORed for the set bits of v
+ * (MSB first), as compute_toeplitz_hash accumulates them (tcp_api.c:593-601) */
+static uint32_t toeplitz_byte(const uint8_t *key, int i, unsigned v)
+{
+	uint64_t k40 = ((uint64_t)key[i] << 32) | ((uint64_t)key[i + 1] << 24) |
+		       ((uint64_t)key[i + 2] << 16) | ((uint64_t)key[i + 3] << 8) | key[i + 4];
+	uint32_t r = 0;
+	for (int j = 0; j < 8; j++)
+		if (v & (0x80u >> j))
+			r ^= (uint32_t)(k40 >> (8 - j));
+	return r;
+}
+
+/* tuple byte i (Toeplitz order: src ip, dst ip, sport, dport; wire bytes)
+ * -> byte position in tcp_to_idx's 24-byte crc32q stream: w1 = local (dst)
+ * ip, w2 = remote (src) ip, w3 = (dport<<16 | sport) host order, sign-extended */
+static const int k_crc_pos[12] = {8, 9, 10, 11, 0, 1, 2, 3, 17, 16, 19, 18};
+
+int ixg_rx_hash_tables(const struct ixg_rx_cfg *cfg, uint64_t *tab, uint32_t *crc_const)
+{
+	if (!cfg || !tab)
+		return -EINVAL;
+	uint8_t s[24];
+	memset(s, 0, sizeof(s));
+	if (crc_const)
+		*crc_const = crc_stream(IXG_PCB_HASH_SEED, s);
+	for (int i = 0; i < 12; i++)
+		for (unsigned v = 0; v < 256; v++) {
+			memset(s, 0, sizeof(s));
+			s[k_crc_pos[i]] = (uint8_t)v;
+			if (i == 10 && (v & 0x80)) /* dport's high byte is the int's sign */
+				memset(s + 20, 0xff, 4);
+			uint64_t crc = crc_stream(0, s);
+			tab[i * 256 + v] = (uint64_t)toeplitz_byte(cfg->rss_key, i, v) | (crc << 32);
+		}
+	return 0;
+}
+
+static void hash_table6(const struct ixg_rx_cfg *cfg, uint32_t *tab6)
+{
+	for (int i = 0; i < 36; i++)
+		for (unsigned v = 0; v < 256; v++)
+			tab6[i * 256 + v] = toeplitz_byte(cfg->rss_key, i, v);
+}
+
+/* ---- context -------------------------------------------------------------- */
+
+int ixg_abi_version(void) { return IXGRX_ABI_VERSION; }
+
+const char *ixg_strerror(int err)
+{
+	switch (err) {
+	case 0: return "ok";
+	case -EINVAL: return "invalid argument";
+	case -ENOMEM: return "out of memory";
+	case -ENODEV: return "no such HIP device";
+	case -EIO: return "HIP runtime error";
+	default: return "unknown error";
+	}
+}
+
+#define HIPCHK(x)                       \
+	do {                            \
+		if ((x) != hipSuccess)  \
+			return -EIO;    \
+	} while (0)
+
+void ixg_rx_fini(void *vctx)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c)
+		return;
+	hipSetDevice(c->device);
+	if (c->stream)
+		hipStreamSynchronize(c->stream);
+	hipFree(c->d_tab);
+	hipFree(c->d_tab6);
+	hipFree(c->d_frames);
+	hipFree(c->d_off);
+	hipFree(c->d_len);
+	hipFree(c->d_out);
+	hipFree(c->d_csum);
+	hipHostFree(c->h_frames);
+	hipHostFree(c->h_off);
+	hipHostFree(c->h_len);
+	if (c->stream)
+		hipStreamDestroy(c->stream);
+	free(c);
+}
+
+int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
+{
+	if (!cfg || !out)
+		return -EINVAL;
+	*out = NULL;
+	if (cfg->nb_rx_fgs == 0 || cfg->nb_rx_fgs > IXG_ETH_MAX_NUM_FG ||
+	    (cfg->nb_rx_fgs & (cfg->nb_rx_fgs - 1)))
+		return -EINVAL;
+	if ((uint32_t)cfg->dev_idx * IXG_ETH_MAX_NUM_FG + IXG_ETH_MAX_NUM_FG > 0x10000u)
+		return -EINVAL;
+	if (cfg->flags & ~(uint32_t)(IXG_F_NO_CSUM_DROP | IXG_F_IPV6))
+		return -EINVAL;
+	int ndev = 0;
+	if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+		return -ENODEV;
+	struct ixg_ctx *c = (struct ixg_ctx *)calloc(1, sizeof(*c));
+	if (!c)
+		return -ENOMEM;
+	c->device = device;
+	c->cfg = *cfg;
+	int rc = -EIO;
+	if (hipSetDevice(device) != hipSuccess)
+		goto fail;
+	hipDeviceProp_t prop;
+	if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+		goto fail;
+	c->grid_max = (uint32_t)prop.multiProcessorCount * (uint32_t)ixgrx_blocks_per_cu();
+	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
+	if (!tab) {
+		rc = -ENOMEM;
+		goto fail;
+	}
+	ixg_rx_hash_tables(cfg, tab, &c->crc_const);
+	if (hipMalloc((void **)&c->d_tab, 12 * 256 * sizeof(uint64_t)) != hipSuccess ||
+	    hipMemcpy(c->d_tab, tab, 12 * 256 * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+		free(tab);
+		goto fail;
+	}
+	free(tab);
+	if (cfg->flags & IXG_F_IPV6) {
+		uint32_t *t6 = (uint32_t *)malloc(36 * 256 * sizeof(uint32_t));
+		if (!t6) {
+			rc = -ENOMEM;
+			goto fail;
+		}
+		hash_table6(cfg, t6);
+		if (hipMalloc((void **)&c->d_tab6, 36 * 256 * sizeof(uint32_t)) != hipSuccess ||
+		    hipMemcpy(c->d_tab6, t6, 36 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+			free(t6);
+			goto fail;
+		}
+		free(t6);
+	}
+	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+		goto fail;
+	*out = c;
+	return 0;
+fail:
+	ixg_rx_fini(c);
+	return rc;
+}
+
+/* ---- batches --------------------------------------------------------------- */
+
+static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
+		  uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum, hipStream_t s)
+{
+	struct ixg_kparams p;
+	memset(&p, 0, sizeof(p));
+	p.base = base;
+	p.off = off;
+	p.len = len;
+	p.out = out;
+	p.csum = csum;
+	p.tab = c->d_tab;
+	p.tab6 = c->d_tab6;
+	p.stride = stride;
+	p.n = n;
+	p.crc_const = c->crc_const;
+	p.flags = c->cfg.flags;
+	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
+	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
+	uint32_t blk = ixgrx_block();
+	uint64_t want = ((uint64_t)n + blk - 1) / blk;
+	uint32_t grid = want < c->grid_max ? (uint32_t)want : c->grid_max;
+	if (grid == 0)
+		grid = 1;
+	return ixgrx_launch(&p, grid, s) == 0 ? 0 : -EIO;
+}
+
+int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
+		     ixg_csum_t *d_csum, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || (n && (!fr->base || !fr->len || !d_out)))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)fr->base & 3) || (!fr->off && (fr->stride & 3)) || ((uintptr_t)d_out & 15) ||
+	    ((uintptr_t)fr->len & 1) || ((uintptr_t)fr->off & 7) || ((uintptr_t)d_csum & 3))
+		return -EINVAL;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -EIO;
+	return launch(c, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, d_csum,
+		      (hipStream_t)stream);
+}
+
+static int grow_dev(struct ixg_ctx *c, size_t bytes, size_t n)
+{
+	if (bytes > c->d_frames_cap) {
+		hipFree(c->d_frames);
+		c->d_frames = NULL;
+		size_t cap = bytes + bytes / 4 + 4096;
+		HIPCHK(hipMalloc((void **)&c->d_frames, cap));
+		c->d_frames_cap = cap;
+	}
+	if (n > c->d_n_cap) {
+		hipFree(c->d_off);
+		hipFree(c->d_len);
+		hipFree(c->d_out);
+		hipFree(c->d_csum);
+		c->d_off = NULL;
+		c->d_len = NULL;
+		c->d_out = NULL;
+		c->d_csum = NULL;
+		size_t cap = n + n / 4 + 64;
+		HIPCHK(hipMalloc((void **)&c->d_off, cap * sizeof(uint64_t)));
+		HIPCHK(hipMalloc((void **)&c->d_len, cap * sizeof(uint16_t)));
+		HIPCHK(hipMalloc((void **)&c->d_out, cap * sizeof(struct ixg_rx_rec)));
+		HIPCHK(hipMalloc((void **)&c->d_csum, cap * sizeof(uint32_t)));
+		c->d_n_cap = cap;
+	}
+	return 0;
+}
+
+int ixg_rx_batch_host(void *vctx, const void *frames, const uint64_t *off, const uint16_t *len,
+		      uint32_t stride, uint32_t n, struct ixg_rx_rec *out, ixg_csum_t *csum)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && (!frames || !len || !out)))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)frames & 3) || (!off && (stride & 3)))
+		return -EINVAL;
+	uint64_t end = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		uint64_t o = off ? off[i] : (uint64_t)i * stride;
+		if (o & 3)
+			return -EINVAL;
+		if (o + len[i] > end)
+			end = o + len[i];
+	}
+	/* the caller's buffer need not have IXG_TAIL_PAD: copy what exists and
+	 * leave the device copy padded */
+	HIPCHK(hipSetDevice(c->device));
+	int rc = grow_dev(c, (size_t)end + IXG_TAIL_PAD, n);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(c->d_frames, frames, (size_t)end, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemsetAsync(c->d_frames + end, 0, IXG_TAIL_PAD, c->stream));
+	if (off)
+		HIPCHK(hipMemcpyAsync(c->d_off, off, n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->d_len, len, n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+	rc = launch(c, c->d_frames, off ? c->d_off : NULL, c->d_len, stride, n, c->d_out,
+		    csum ? c->d_csum : NULL, c->stream);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(out, c->d_out, n * sizeof(*out), hipMemcpyDeviceToHost, c->stream));
+	if (csum)
+		HIPCHK(hipMemcpyAsync(csum, c->d_csum, n * sizeof(*csum), hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+static int grow_host(struct ixg_ctx *c, size_t bytes, size_t n)
+{
+	if (bytes > c->h_frames_cap) {
+		hipHostFree(c->h_frames);
+		c->h_frames = NULL;
+		size_t cap = bytes + bytes / 4 + 4096;
+		HIPCHK(hipHostMalloc((void **)&c->h_frames, cap, hipHostMallocDefault));
+		c->h_frames_cap = cap;
+	}
+	if (n > c->h_n_cap) {
+		hipHostFree(c->h_off);
+		hipHostFree(c->h_len);
+		c->h_off = NULL;
+		c->h_len = NULL;
+		size_t cap = n + n / 4 + 64;
+		HIPCHK(hipHostMalloc((void **)&c->h_off, cap * sizeof(uint64_t), hipHostMallocDefault));
+		HIPCHK(hipHostMalloc((void **)&c->h_len, cap * sizeof(uint16_t), hipHostMallocDefault));
+		c->h_n_cap = cap;
+	}
+	return 0;
+}
+
+int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx_rec *out)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && (!mbufs || !out)))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	/* gather: frame = mbuf + 64, L = mbuf->len (size_t @0), inc/ix/mbuf.h:73-90 */
+	size_t total = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		size_t l;
+		memcpy(&l, mbufs[i], sizeof(l));
+		if (l > 0xffff)
+			return -EINVAL;
+		total += (l + 3) & ~(size_t)3;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	int rc = grow_host(c, total + IXG_TAIL_PAD, n);
+	if (!rc)
+		rc = grow_dev(c, total + IXG_TAIL_PAD, n);
+	if (rc)
+		return rc;
+	size_t o = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint8_t *m = (const uint8_t *)mbufs[i];
+		size_t l;
+		memcpy(&l, m, sizeof(l));
+		memcpy(c->h_frames + o, m + IXG_MBUF_HEADER_LEN, l);
+		memset(c->h_frames + o + l, 0, ((l + 3) & ~(size_t)3) - l);
+		c->h_off[i] = o;
+		c->h_len[i] = (uint16_t)l;
+		o += (l + 3) & ~(size_t)3;
+	}
+	memset(c->h_frames + o, 0, IXG_TAIL_PAD);
+	HIPCHK(hipMemcpyAsync(c->d_frames, c->h_frames, o + IXG_TAIL_PAD, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->d_off, c->h_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->d_len, c->h_len, n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+	rc = launch(c, c->d_frames, c->d_off, c->d_len, 0, n, c->d_out, NULL, c->stream);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(out, c->d_out, n * sizeof(*out), hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+/* ---- dispatch: what eth_process_recv does per packet, from records ------ */
+
+uint32_t ixg_rx_dispatch(void *const *mbufs, const struct ixg_rx_rec *recs, uint32_t n,
+			 const struct ixg_rx_ops *ops, void *user)
+{
+	uint32_t delivered = 0;
+	if (!ops)
+		return 0;
+	for (uint32_t i = 0; i < n; i++) {
+		const struct ixg_rx_rec *r = &recs[i];
+		void (*fn)(void *, void *, const struct ixg_rx_rec *) = ops->drop;
+		switch (r->verdict) {
+		case IXG_V_TCP:
+		case IXG_V_TCP6:
+			fn = ops->tcp; /* tcp_input_tmp -> tcp_input body (ip.c:93-96) */
+			break;
+		case IXG_V_UDP:
+		case IXG_V_UDP6:
+			fn = ops->udp; /* udp_input (ip.c:97-100) */
+			break;
+		case IXG_V_ICMP_ECHO:
+			fn = ops->icmp_echo; /* icmp_input -> icmp_reflect (icmp.c:89-92) */
+			break;
+		case IXG_V_ARP:
+			fn = ops->arp; /* arp_input (ip.c:134-135) */
+			break;
+		default:
+			break;
+		}
+		if (r->verdict < 0x80)
+			delivered++;
+		if (fn)
+			fn(user, mbufs ? mbufs[i] : NULL, r);
+	}
+	return delivered;
+}

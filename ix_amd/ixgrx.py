@@ -1,0 +1,203 @@
+"""ctypes binding of the C ABI in include/ixgrx.h (ix_amd/libixgrx.so).
+
+This is the host-side mirror of the drop-in boundary: ``RxEngine`` wraps one
+``ixg_rx_init`` context (one per host thread, IX's per-CPU model) and exposes
+the three batch entry points. PyTorch, when used, only supplies device
+memory and streams; nothing here falls back to a CPU path: if the HIP
+library is missing, importing the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libixgrx.so")
+
+ABI_VERSION = 1
+IXG_F_NO_CSUM_DROP = 1 << 0
+IXG_F_IPV6 = 1 << 1
+IXG_TAIL_PAD = 64
+IXG_NO_BUCKET = 0xFFFF
+
+# struct ixg_rx_rec (16 bytes)
+REC_DTYPE = np.dtype([
+    ("fg_id", "<u2"), ("verdict", "u1"), ("flags", "u1"), ("l4_off", "<u2"), ("l4_len", "<u2"),
+    ("rss_hash", "<u4"), ("pcb_bucket", "<u2"), ("tcp_flags", "u1"), ("rsvd", "u1"),
+])
+assert REC_DTYPE.itemsize == 16
+
+VERDICTS = {
+    0x01: "TCP", 0x02: "UDP", 0x03: "ICMP_ECHO", 0x04: "ARP", 0x05: "TCP6", 0x06: "UDP6",
+    0x80: "DROP_ETHERTYPE", 0x81: "DROP_IP_SHORT", 0x82: "DROP_IP_VERSION", 0x83: "DROP_IP_IHL",
+    0x84: "DROP_IP_FRAG", 0x85: "DROP_IP_LEN", 0x86: "DROP_IP_TRUNC", 0x87: "DROP_IP_PROTO",
+    0x88: "DROP_TCP_SHORT", 0x89: "DROP_TCP_HDRLEN", 0x8A: "DROP_UDP_LEN", 0x8B: "DROP_ICMP_SHORT",
+    0x8C: "DROP_ICMP_CSUM", 0x8D: "DROP_ICMP_TYPE", 0x8E: "DROP_CSUM_IP", 0x8F: "DROP_CSUM_L4",
+    0x90: "DROP_IP6",
+}
+V = {name: code for code, name in VERDICTS.items()}
+
+RF_IP_CSUM_CHECKED, RF_IP_CSUM_OK, RF_L4_CSUM_CHECKED, RF_L4_CSUM_OK, RF_RSS = 1, 2, 4, 8, 16
+
+# symbols include/ixgrx.h declares (checked by tests/test_abi.py)
+EXPORTS = (
+    "ixg_rx_init", "ixg_rx_fini", "ixg_rx_batch_dev", "ixg_rx_batch_mbufs", "ixg_rx_batch_host",
+    "ixg_rx_hash_tables", "ixg_abi_version", "ixg_strerror", "ixg_rx_dispatch",
+)
+
+
+class RxCfg(ctypes.Structure):
+    _fields_ = [("rss_key", ctypes.c_uint8 * 40), ("nb_rx_fgs", ctypes.c_uint16),
+                ("dev_idx", ctypes.c_uint16), ("flags", ctypes.c_uint32)]
+
+
+class RxFrames(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
+                ("stride", ctypes.c_uint32), ("rsvd", ctypes.c_uint32)]
+
+
+@dataclass
+class Config:
+    rss_key: bytes = bytes(40)
+    nb_rx_fgs: int = 128
+    dev_idx: int = 0
+    flags: int = 0
+
+    def to_c(self) -> RxCfg:
+        c = RxCfg()
+        if len(self.rss_key) != 40:
+            raise ValueError("rss_key must be 40 bytes")
+        ctypes.memmove(c.rss_key, self.rss_key, 40)
+        c.nb_rx_fgs = self.nb_rx_fgs
+        c.dev_idx = self.dev_idx
+        c.flags = self.flags
+        return c
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libixgrx.so; raises if it has not been built (no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} missing: build it with __graft_entry__.build() "
+                           "(make -C ix_amd/csrc)")
+    lib = ctypes.CDLL(path)
+    vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    lib.ixg_rx_init.argtypes = [ctypes.POINTER(RxCfg), i32, ctypes.POINTER(vp)]
+    lib.ixg_rx_init.restype = i32
+    lib.ixg_rx_fini.argtypes = [vp]
+    lib.ixg_rx_fini.restype = None
+    lib.ixg_rx_batch_dev.argtypes = [vp, ctypes.POINTER(RxFrames), u32, vp, vp, vp]
+    lib.ixg_rx_batch_dev.restype = i32
+    lib.ixg_rx_batch_mbufs.argtypes = [vp, vp, u32, vp]
+    lib.ixg_rx_batch_mbufs.restype = i32
+    lib.ixg_rx_batch_host.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp]
+    lib.ixg_rx_batch_host.restype = i32
+    lib.ixg_rx_hash_tables.argtypes = [ctypes.POINTER(RxCfg), vp, ctypes.POINTER(u32)]
+    lib.ixg_rx_hash_tables.restype = i32
+    lib.ixg_abi_version.argtypes = []
+    lib.ixg_abi_version.restype = i32
+    lib.ixg_strerror.argtypes = [i32]
+    lib.ixg_strerror.restype = ctypes.c_char_p
+    lib.ixg_rx_dispatch.argtypes = [vp, vp, u32, vp, vp]
+    lib.ixg_rx_dispatch.restype = u32
+    if lib.ixg_abi_version() != ABI_VERSION:
+        raise RuntimeError("libixgrx ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load_library().ixg_strerror(rc).decode()
+        raise RuntimeError(f"{what} failed: {rc} ({msg})")
+
+
+def hash_tables(cfg: Config) -> tuple[np.ndarray, int]:
+    """The combined Toeplitz/CRC byte tables the kernels use (host-built)."""
+    lib = load_library()
+    tab = np.zeros(12 * 256, dtype=np.uint64)
+    cc = ctypes.c_uint32(0)
+    c = cfg.to_c()
+    _check(lib.ixg_rx_hash_tables(ctypes.byref(c), tab.ctypes.data, ctypes.byref(cc)), "ixg_rx_hash_tables")
+    return tab.reshape(12, 256), int(cc.value)
+
+
+@dataclass
+class RxEngine:
+    """One ixg_rx context on HIP device `device`."""
+    cfg: Config
+    device: int = 0
+    _ctx: ctypes.c_void_p = field(default_factory=ctypes.c_void_p, init=False)
+
+    def __post_init__(self):
+        lib = load_library()
+        self._ccfg = self.cfg.to_c()
+        _check(lib.ixg_rx_init(ctypes.byref(self._ccfg), self.device, ctypes.byref(self._ctx)), "ixg_rx_init")
+
+    def close(self) -> None:
+        if self._ctx:
+            load_library().ixg_rx_fini(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch_dev(self, base: int, off: int | None, length: int, stride: int, n: int, out: int,
+                  csum: int | None = None, stream: int | None = None) -> None:
+        """Device-resident batch: all arguments are device pointers (ints)."""
+        fr = RxFrames(base, off or None, length, stride, 0)
+        _check(load_library().ixg_rx_batch_dev(self._ctx, ctypes.byref(fr), n, out, csum or None,
+                                               stream or None), "ixg_rx_batch_dev")
+
+    def batch_host(self, blob: np.ndarray, off: np.ndarray | None, lens: np.ndarray, stride: int = 0,
+                   want_csum: bool = False):
+        """Host batch: copies in, runs, copies records (and residuals) back."""
+        n = int(lens.shape[0])
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint16)
+        offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+        rec = np.zeros(n, dtype=REC_DTYPE)
+        cs = np.zeros(n, dtype=np.uint32) if want_csum else None
+        _check(load_library().ixg_rx_batch_host(
+            self._ctx, blob.ctypes.data, None if offa is None else offa.ctypes.data, lens.ctypes.data,
+            stride, n, rec.ctypes.data, None if cs is None else cs.ctypes.data), "ixg_rx_batch_host")
+        return (rec, cs) if want_csum else rec
+
+    def batch_trace(self, tr, want_csum: bool = False):
+        return self.batch_host(tr.blob, tr.off, tr.len, tr.stride, want_csum)
+
+    def batch_mbufs(self, mbuf_ptrs: np.ndarray) -> np.ndarray:
+        """IX layout: array of host mbuf addresses (len @0, data @+64)."""
+        ptrs = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        n = int(ptrs.shape[0])
+        rec = np.zeros(n, dtype=REC_DTYPE)
+        _check(load_library().ixg_rx_batch_mbufs(self._ctx, ptrs.ctypes.data, n, rec.ctypes.data),
+               "ixg_rx_batch_mbufs")
+        return rec
+
+
+def make_mbufs(tr) -> tuple[np.ndarray, np.ndarray]:
+    """Lay a trace out as IX mbufs (2112-B elements, len @0, data @+64).
+    Returns (arena, pointer array); keep the arena alive while using pointers."""
+    n = tr.n
+    arena = np.zeros(n * 2112 + 64, dtype=np.uint8)
+    base = (-arena.ctypes.data) % 64
+    offs = tr.offsets()
+    for i in range(n):
+        o = base + i * 2112
+        L = int(tr.len[i])
+        arena[o:o + 8] = np.frombuffer(np.uint64(L).tobytes(), np.uint8)
+        arena[o + 64:o + 64 + L] = tr.blob[int(offs[i]):int(offs[i]) + L]
+    ptrs = arena.ctypes.data + base + np.arange(n, dtype=np.uint64) * 2112
+    return arena, ptrs

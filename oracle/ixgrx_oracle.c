@@ -1,0 +1,618 @@
+/*
+ * ixgrx_oracle.c - CPU restatement of IX's RX per-packet transform.
+ *
+ * TEST INFRASTRUCTURE ONLY (see ixgrx_oracle.h). Every function cites the
+ * reference file:line it restates (paths relative to /root/reference).
+ * Pinned against golden vectors from the reference's own code
+ * (tests/golden/*.npz, made by tests/golden/make_golden.py through
+ * oracle/ref_harness) and against the public RSS verification vectors.
+ *
+ * Semantics that live in NIC silicon rather than in the tree (IX offloads
+ * the IP/L4 checksum verdict and the RSS hash to the 82599) are stated in
+ * DESIGN.md "NIC rules"; they are the same rules the harness applies, and
+ * are marked [NIC] below.
+ */
+#include "ixgrx_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define FOLD_U32T(u) (((u) >> 16) + ((u)&0x0000ffffUL)) /* inc/lwip/lwip/inet_chksum.h:76 */
+#define SWAP_BYTES_IN_WORD(w) ((((w)&0xff) << 8) | (((w)&0xff00) >> 8)) /* :70 */
+
+static inline uint64_t ld64(const uint8_t *p)
+{
+	uint64_t v;
+	memcpy(&v, p, 8);
+	return v; /* x86-64 and gfx950 are little-endian, as the reference assumes */
+}
+static inline uint32_t ld32(const uint8_t *p)
+{
+	uint32_t v;
+	memcpy(&v, p, 4);
+	return v;
+}
+static inline uint16_t ld16(const uint8_t *p)
+{
+	uint16_t v;
+	memcpy(&v, p, 2);
+	return v;
+}
+static inline uint16_t bswap16(uint16_t x) { return (uint16_t)((x >> 8) | (x << 8)); }
+
+/*
+ * chksum_internet (inc/asm/chksum.h:40-95): an adc chain over 8-byte LE
+ * words (the carry threads through the loop because `dec` keeps CF), one
+ * trailing adc $0, then 4/2/1-byte tails each with add+adc $0, a 64->32 fold
+ * with one end-around carry, a 32->16 fold with one end-around carry, and
+ * the complement. Restated step by step, carries included.
+ */
+uint16_t ixgo_chksum_internet(const uint8_t *buf, int len)
+{
+	uint64_t sum = 0;
+	unsigned cf = 0; /* xorq clears CF */
+	uint32_t n8 = (uint32_t)len >> 3;
+
+	if (n8) {
+		for (uint32_t i = 0; i < n8; i++) { /* 1: adcq (%1), %0 */
+			uint64_t v = ld64(buf);
+			uint64_t t = sum + v;
+			unsigned c1 = t < sum;
+			uint64_t t2 = t + cf;
+			unsigned c2 = t2 < t;
+			sum = t2;
+			cf = c1 | c2;
+			buf += 8;
+		}
+		sum += cf; /* adcq $0, %0 (carry-out provably 0) */
+	}
+	if ((uint32_t)len & 4) { /* 2: */
+		uint64_t t = sum + ld32(buf);
+		sum = t + (t < sum);
+		buf += 4;
+	}
+	if ((uint32_t)len & 2) { /* 3: movzxw */
+		uint64_t t = sum + ld16(buf);
+		sum = t + (t < sum);
+		buf += 2;
+	}
+	if ((uint32_t)len & 1) { /* 4: movzxb */
+		uint64_t t = sum + *buf;
+		sum = t + (t < sum);
+	}
+	/* 5: fold 64 -> 32 (addl + adcl $0) */
+	uint32_t lo = (uint32_t)sum, hi = (uint32_t)(sum >> 32);
+	uint32_t s32 = hi + lo;
+	s32 += (s32 < lo);
+	/* fold 32 -> 16 (shrl $16; addw; adcw $0) */
+	uint16_t a = (uint16_t)(s32 >> 16), b = (uint16_t)s32;
+	uint16_t w = (uint16_t)(a + b);
+	w = (uint16_t)(w + (w < b));
+	return (uint16_t)~w;
+}
+
+/*
+ * lwip_standard_chksum, LWIP_CHKSUM_ALGORITHM 2 (dp/lwip/inet_chksum.c:158-198):
+ * 16-bit adds into a u32, odd start address handled by byte-swapping.
+ */
+uint16_t ixgo_standard_chksum(const void *dataptr, int len)
+{
+	const uint8_t *pb = (const uint8_t *)dataptr;
+	uint16_t t = 0;
+	uint32_t sum = 0;
+	int odd = ((uintptr_t)pb & 1);
+
+	if (odd && len > 0) {
+		((uint8_t *)&t)[1] = *pb++;
+		len--;
+	}
+	const uint8_t *ps = pb;
+	while (len > 1) {
+		sum += ld16(ps);
+		ps += 2;
+		len -= 2;
+	}
+	if (len > 0)
+		((uint8_t *)&t)[0] = *ps;
+	sum += t;
+	sum = FOLD_U32T(sum);
+	sum = FOLD_U32T(sum);
+	if (odd)
+		sum = SWAP_BYTES_IN_WORD(sum);
+	return (uint16_t)sum;
+}
+
+/*
+ * inet_cksum_pseudo_partial_base (inet_chksum.c:398-440) over a single
+ * PBUF_ROM pbuf {payload = seg, len = seg_len} -- the shape tcp_input_tmp
+ * builds (dp/lwip/misc.c:61-62) -- with chksum_len = seg_len.
+ */
+static uint16_t pseudo_partial_base(const uint8_t *seg, uint16_t seg_len, uint8_t proto,
+				    uint16_t proto_len, uint32_t acc)
+{
+	uint16_t chksum_len = seg_len;
+	uint8_t swapped = 0;
+
+	if (chksum_len > 0) { /* for (q = p; q && chksum_len > 0; q = q->next), one pbuf */
+		uint16_t chklen = seg_len;
+		if (chklen > chksum_len)
+			chklen = chksum_len;
+		acc += ixgo_standard_chksum(seg, chklen);
+		acc = FOLD_U32T(acc);
+		if (seg_len % 2 != 0) {
+			swapped = 1 - swapped;
+			acc = SWAP_BYTES_IN_WORD(acc);
+		}
+	}
+	if (swapped)
+		acc = SWAP_BYTES_IN_WORD(acc);
+	acc += (uint32_t)bswap16((uint16_t)proto); /* htons on LE */
+	acc += (uint32_t)bswap16(proto_len);
+	acc = FOLD_U32T(acc);
+	acc = FOLD_U32T(acc);
+	return (uint16_t)~(acc & 0xffffUL);
+}
+
+/* inet_chksum_pseudo_partial (inet_chksum.c:454-472) */
+uint16_t ixgo_pseudo_partial(const uint8_t *seg, uint16_t seg_len, uint8_t proto,
+			     uint16_t proto_len, uint32_t src_raw, uint32_t dst_raw)
+{
+	uint32_t acc = (src_raw & 0xffffUL);
+	acc += ((src_raw >> 16) & 0xffffUL);
+	acc += (dst_raw & 0xffffUL);
+	acc += ((dst_raw >> 16) & 0xffffUL);
+	acc = FOLD_U32T(acc);
+	acc = FOLD_U32T(acc);
+	return pseudo_partial_base(seg, seg_len, proto, proto_len, acc);
+}
+
+/* ip6_chksum_pseudo_partial (inet_chksum.c:488-509) */
+uint16_t ixgo_pseudo6_partial(const uint8_t *seg, uint16_t seg_len, uint8_t proto,
+			      uint16_t proto_len, const uint8_t src[16], const uint8_t dst[16])
+{
+	uint32_t acc = 0;
+	for (int k = 0; k < 4; k++) {
+		uint32_t a = ld32(src + 4 * k);
+		acc += (a & 0xffffUL);
+		acc += ((a >> 16) & 0xffffUL);
+		a = ld32(dst + 4 * k);
+		acc += (a & 0xffffUL);
+		acc += ((a >> 16) & 0xffffUL);
+	}
+	acc = FOLD_U32T(acc);
+	acc = FOLD_U32T(acc);
+	return pseudo_partial_base(seg, seg_len, proto, proto_len, acc);
+}
+
+/*
+ * compute_toeplitz_hash (dp/net/tcp_api.c:581-604), bit-serial, generalised
+ * from the fixed 12-byte input to n bytes (n = 36 for the IPv6 extension;
+ * key bytes used: 4 + n).
+ */
+uint32_t ixgo_toeplitz(const uint8_t *key, const uint8_t *input, int n)
+{
+	uint32_t result = 0;
+	uint32_t key_part = ((uint32_t)key[0] << 24) | ((uint32_t)key[1] << 16) |
+			    ((uint32_t)key[2] << 8) | key[3]; /* htonl(((u32 *)key)[0]) */
+	for (int i = 0; i < n; i++) {
+		for (int j = 128; j; j >>= 1) {
+			if (input[i] & j)
+				result ^= key_part;
+			key_part <<= 1;
+			if (key[i + 4] & j)
+				key_part |= 1;
+		}
+	}
+	return result;
+}
+
+/* crc32q (inc/ix/hash.h:35-39): CRC-32C, reflected poly 0x82F63B78, no
+ * pre/post inversion, 8 operand bytes consumed least significant first. */
+uint32_t ixgo_crc32c_u64(uint32_t crc, uint64_t val)
+{
+	for (int k = 0; k < 8; k++) {
+		crc ^= (uint32_t)((val >> (8 * k)) & 0xff);
+		for (int b = 0; b < 8; b++)
+			crc = (crc >> 1) ^ (0x82F63B78u & (0u - (crc & 1u)));
+	}
+	return crc;
+}
+
+/*
+ * tcp_to_idx (inc/lwip/lwip/tcp_impl.h:381-387) with hash_crc32c_two/one
+ * (inc/ix/hash.h:51-71). The address words are the raw network-order u32s;
+ * the port word is the int expression (local_port << 16) | remote_port,
+ * which sign-extends into the upper 32 bits of the crc32q operand when
+ * local_port >= 0x8000.
+ */
+uint16_t ixgo_tcp_to_idx(uint32_t local_raw, uint32_t remote_raw, uint16_t local_port,
+			 uint16_t remote_port)
+{
+	int idx = (int)ixgo_crc32c_u64(ixgo_crc32c_u64(IXG_PCB_HASH_SEED, (uint64_t)local_raw),
+				       (uint64_t)remote_raw);
+	int32_t word = (int32_t)(((uint32_t)local_port << 16) | remote_port);
+	idx = (int)ixgo_crc32c_u64((uint32_t)idx, (uint64_t)(int64_t)word);
+	idx &= IXG_PCB_BUCKETS - 1;
+	return (uint16_t)idx;
+}
+
+/* ---- table-driven hashes (CPU-baseline fast mode) -------------------- */
+
+/* Both hashes are GF(2)-affine in the 12 tuple bytes, so a byte table
+ * T[pos][v] = {toeplitz contribution, crc contribution} reproduces them:
+ * tuple byte order = Toeplitz input order (src ip, dst ip, sport, dport). */
+struct hashtab {
+	uint32_t toep[12][256];
+	uint32_t crc[12][256];
+	uint32_t crc_const;
+};
+
+/* crc stream position (0..23 = words w1 w2 w3 of tcp_to_idx) of tuple byte i */
+static const int crc_pos[12] = {8, 9, 10, 11, 0, 1, 2, 3, 17, 16, 19, 18};
+
+static uint32_t crc_stream(uint32_t seed, const uint8_t s[24])
+{
+	return ixgo_crc32c_u64(ixgo_crc32c_u64(ixgo_crc32c_u64(seed, ld64(s)), ld64(s + 8)), ld64(s + 16));
+}
+
+static void hashtab_build(struct hashtab *h, const uint8_t *key)
+{
+	uint8_t zero24[24] = {0};
+	h->crc_const = crc_stream(IXG_PCB_HASH_SEED, zero24);
+	for (int i = 0; i < 12; i++)
+		for (int v = 0; v < 256; v++) {
+			uint8_t in[12] = {0}, s[24] = {0};
+			in[i] = (uint8_t)v;
+			h->toep[i][v] = ixgo_toeplitz(key, in, 12);
+			s[crc_pos[i]] = (uint8_t)v;
+			if (i == 10 && (v & 0x80)) /* dport high byte: sign extension */
+				memset(s + 20, 0xff, 4);
+			h->crc[i][v] = crc_stream(0, s);
+		}
+}
+
+/* ---- the per-frame transform ----------------------------------------- */
+
+struct frame {
+	const uint8_t *p;
+	uint32_t len;
+};
+/* bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L") */
+static inline uint8_t B(const struct frame *f, uint32_t i) { return i < f->len ? f->p[i] : 0; }
+static inline uint16_t B16(const struct frame *f, uint32_t i)
+{
+	return (uint16_t)((B(f, i) << 8) | B(f, i + 1));
+}
+static inline uint32_t Braw32(const struct frame *f, uint32_t i)
+{
+	return (uint32_t)B(f, i) | ((uint32_t)B(f, i + 1) << 8) | ((uint32_t)B(f, i + 2) << 16) |
+	       ((uint32_t)B(f, i + 3) << 24);
+}
+
+static void set_drop(struct ixg_rx_rec *r, uint8_t v)
+{
+	r->verdict = v;
+	r->l4_off = 0;
+	r->l4_len = 0;
+	r->pcb_bucket = IXG_NO_BUCKET;
+	r->tcp_flags = 0;
+}
+
+static void rx_one(const struct ixg_rx_cfg *cfg, const struct hashtab *ht, const uint8_t *frame,
+		   uint32_t L, struct ixg_rx_rec *r, uint32_t *csum, int work)
+{
+	struct frame fr = {frame, L}, *f = &fr;
+	uint32_t rss = 0;
+	uint16_t ip_res = 0xffff, l4_res = 0xffff;
+	uint8_t flags = 0;
+	int full = (work == IXGO_WORK_FULL);
+
+	memset(r, 0, sizeof(*r));
+	r->pcb_bucket = IXG_NO_BUCKET;
+
+	uint16_t etype = B16(f, 12);                     /* ip.c:132 ethhdr->type */
+	int v6 = (etype == 0x86DD) && (cfg->flags & IXG_F_IPV6);
+	uint8_t vh = B(f, 14);
+	uint32_t ihl = vh & 15, ver = vh >> 4;           /* inc/net/ip.h:84-90 LE bitfield */
+	uint32_t ip_len = B16(f, 16);                    /* ip.c:82 */
+	uint16_t ip_off = B16(f, 20);                    /* ip.c:78 */
+	uint8_t proto = B(f, 23);
+	int frag = (ip_off & 0x3FFF) != 0;               /* IP_OFFMASK | IP_MF */
+	uint32_t l4 = 14 + ihl * 4;
+
+	/* [NIC] the IPv4 header checksum is verified when the whole header is present */
+	int hdr_ok = etype == 0x0800 && ver == 4 && ihl >= 5 && l4 <= L;
+	if (full && hdr_ok) {
+		ip_res = ixgo_chksum_internet(frame + 14, (int)(ihl * 4));
+		flags |= IXG_RF_IP_CSUM_CHECKED | (ip_res == 0 ? IXG_RF_IP_CSUM_OK : 0);
+	}
+
+	/* [NIC] RSS Toeplitz over {src, dst, sport, dport}, non-fragmented IPv4
+	 * TCP/UDP only (dp/drivers/common.c:116-134), ports present in the frame */
+	uint8_t tup[36];
+	int tup_n = 0;
+	if (hdr_ok && !frag && (proto == 6 || proto == 17) && l4 + 4 <= L) {
+		for (int i = 0; i < 8; i++)
+			tup[i] = B(f, 26 + i);
+		for (int i = 0; i < 4; i++)
+			tup[8 + i] = B(f, l4 + i);
+		tup_n = 12;
+	} else if (v6 && L >= 58 && (B(f, 14) >> 4) == 6 && (B(f, 20) == 6 || B(f, 20) == 17)) {
+		for (int i = 0; i < 32; i++)
+			tup[i] = B(f, 22 + i);
+		for (int i = 0; i < 4; i++)
+			tup[32 + i] = B(f, 54 + i);
+		tup_n = 36;
+	}
+	if (full && tup_n) {
+		if (tup_n == 12 && ht) {
+			for (int i = 0; i < 12; i++)
+				rss ^= ht->toep[i][tup[i]];
+		} else {
+			rss = ixgo_toeplitz(cfg->rss_key, tup, tup_n);
+		}
+		flags |= IXG_RF_RSS;
+	}
+	/* fg_id = rx_fgs[rss & (nb_rx_fgs-1)].fg_id (ixgbe.c:329-335, init.c:456-462) */
+	r->fg_id = (uint16_t)(cfg->dev_idx * IXG_ETH_MAX_NUM_FG + (rss & (uint32_t)(cfg->nb_rx_fgs - 1)));
+	r->rss_hash = rss;
+
+	/* [NIC] L4 checksum: TCP always, UDP when the checksum field is non-zero
+	 * (RFC 768), over the IP-derived L4 length (what lwIP would pass as
+	 * p->tot_len to inet_chksum_pseudo_partial) */
+	int l4_checked = 0;
+	if (full && hdr_ok && !frag && (proto == 6 || proto == 17) && ip_len >= ihl * 4 &&
+	    14 + ip_len <= L) {
+		uint32_t l4len = ip_len - ihl * 4;
+		if ((proto == 6 && l4len >= 20) || (proto == 17 && l4len >= 8 && B16(f, l4 + 6) != 0)) {
+			l4_res = ixgo_pseudo_partial(frame + l4, (uint16_t)l4len, proto, (uint16_t)l4len,
+						     Braw32(f, 26), Braw32(f, 30));
+			l4_checked = 1;
+		}
+	}
+	uint32_t v6_plen = B16(f, 18);
+	uint8_t v6_nh = B(f, 20);
+	int v6_ok = v6 && L >= 54 && (B(f, 14) >> 4) == 6 && 54 + v6_plen <= L;
+	if (full && v6_ok && ((v6_nh == 6 && v6_plen >= 20) || (v6_nh == 17 && v6_plen >= 8))) {
+		l4_res = ixgo_pseudo6_partial(frame + 54, (uint16_t)v6_plen, v6_nh, (uint16_t)v6_plen,
+					      frame + 22, frame + 38);
+		l4_checked = 1; /* IPv6 UDP checksum is mandatory (RFC 8200 8.1) */
+	}
+	if (l4_checked)
+		flags |= IXG_RF_L4_CSUM_CHECKED | (l4_res == 0 ? IXG_RF_L4_CSUM_OK : 0);
+	r->flags = flags;
+
+	/* the driver drops on the NIC verdict before eth_input (ixgbe.c:312-324,349) */
+	if (!(cfg->flags & IXG_F_NO_CSUM_DROP)) {
+		if ((flags & IXG_RF_IP_CSUM_CHECKED) && !(flags & IXG_RF_IP_CSUM_OK)) {
+			set_drop(r, IXG_V_DROP_CSUM_IP);
+			goto out;
+		}
+		if ((flags & IXG_RF_L4_CSUM_CHECKED) && !(flags & IXG_RF_L4_CSUM_OK)) {
+			set_drop(r, IXG_V_DROP_CSUM_L4);
+			goto out;
+		}
+	}
+
+	/* eth_input (dp/net/ip.c:120-141) */
+	if (etype == 0x0806) { /* ETHTYPE_ARP -> arp_input */
+		r->verdict = IXG_V_ARP;
+		r->l4_off = 14;
+		r->l4_len = (uint16_t)(L >= 14 ? L - 14 : 0);
+		goto out;
+	}
+	if (v6) {
+		/* extension (DESIGN.md "IPv6"): the reference drops ethertype 0x86DD */
+		if (!v6_ok) {
+			set_drop(r, IXG_V_DROP_IP6);
+			goto out;
+		}
+		l4 = 54;
+		ip_len = v6_plen + 40; /* so that l4len below = payload length */
+		ihl = 10;
+		proto = v6_nh;
+		if (proto != 6 && proto != 17) {
+			set_drop(r, IXG_V_DROP_IP6);
+			goto out;
+		}
+		goto l4_dispatch;
+	}
+	if (etype != 0x0800) {
+		set_drop(r, IXG_V_DROP_ETHERTYPE);
+		goto out;
+	}
+	/* ip_input (dp/net/ip.c:63-114) */
+	if (!(14 + 20 <= L)) { set_drop(r, IXG_V_DROP_IP_SHORT); goto out; }  /* :68 */
+	if (ver != 4) { set_drop(r, IXG_V_DROP_IP_VERSION); goto out; }       /* :71 */
+	if (ihl < 5) { set_drop(r, IXG_V_DROP_IP_IHL); goto out; }            /* :74 */
+	if (frag) { set_drop(r, IXG_V_DROP_IP_FRAG); goto out; }              /* :78 */
+	if (ip_len < ihl * 4) { set_drop(r, IXG_V_DROP_IP_LEN); goto out; }   /* :85 */
+	if (!(14 + ip_len <= L)) { set_drop(r, IXG_V_DROP_IP_TRUNC); goto out; } /* :87 */
+
+l4_dispatch:;
+	uint32_t l4len = ip_len - ihl * 4; /* ip.c:90 pktlen -= hdrlen */
+	if (proto == 6) {
+		/* tcp_input_tmp: pbuf len = (u16)(ip_len - ihl*4) (misc.c:61) */
+		uint16_t plen = (uint16_t)l4len;
+		if (plen < 20) { set_drop(r, IXG_V_DROP_TCP_SHORT); goto out; } /* tcp_in.c:189 */
+		uint8_t doff = B(f, l4 + 12) >> 4;        /* TCPH_HDRLEN tcp_impl.h:195 */
+		int inc = -(int)(doff * 4);                /* pbuf_header(p, -(hdrlen*4)) tcp_in.c:222 */
+		if (inc != 0 && (uint16_t)(-inc) > plen) { /* pbuf.c:457-465,498-507 */
+			set_drop(r, IXG_V_DROP_TCP_HDRLEN);
+			goto out;
+		}
+		r->verdict = v6 ? IXG_V_TCP6 : IXG_V_TCP;
+		r->l4_off = (uint16_t)(l4 + doff * 4);
+		r->l4_len = (uint16_t)(plen - doff * 4);
+		r->tcp_flags = B(f, l4 + 13) & 0x3F; /* TCPH_FLAGS, TCP_FLAGS = 0x3f (tcp_in.c:240) */
+		if (!v6) /* idx = tcp_to_idx(dst, src, dest, src) after ntohs (tcp_in.c:230-233) */
+			r->pcb_bucket = ht ? (uint16_t)0 : ixgo_tcp_to_idx(Braw32(f, 30), Braw32(f, 26),
+									 B16(f, l4 + 2), B16(f, l4));
+		if (!v6 && ht) {
+			uint32_t c = ht->crc_const;
+			uint8_t t12[12];
+			for (int i = 0; i < 8; i++)
+				t12[i] = B(f, 26 + i);
+			for (int i = 0; i < 4; i++)
+				t12[8 + i] = B(f, l4 + i);
+			for (int i = 0; i < 12; i++)
+				c ^= ht->crc[i][t12[i]];
+			r->pcb_bucket = (uint16_t)(c & (IXG_PCB_BUCKETS - 1));
+		}
+		goto out;
+	}
+	if (proto == 17) {
+		/* udp_input (dp/net/udp.c:53-89) */
+		uint16_t ulen = B16(f, l4 + 4);
+		if (!(l4 + ulen <= L)) { set_drop(r, IXG_V_DROP_UDP_LEN); goto out; } /* :59 */
+		r->verdict = v6 ? IXG_V_UDP6 : IXG_V_UDP;
+		r->l4_off = (uint16_t)(l4 + 8); /* data = mbuf_nextd(udphdr) :55 */
+		r->l4_len = ulen;               /* usys_udp_recv(..., len, ...) :88 */
+		goto out;
+	}
+	if (proto == 1 && !v6) {
+		/* icmp_input (dp/net/icmp.c:78-115) with len = ip_len - ihl*4 (ip.c:102-104) */
+		if ((int)l4len < 8) { set_drop(r, IXG_V_DROP_ICMP_SHORT); goto out; } /* :80 */
+		uint16_t res = ixgo_chksum_internet(frame + l4, (int)l4len);
+		if (full)
+			l4_res = res;
+		if (res) { set_drop(r, IXG_V_DROP_ICMP_CSUM); goto out; } /* :82 */
+		if (B(f, l4) != 8) { set_drop(r, IXG_V_DROP_ICMP_TYPE); goto out; } /* :88-108 */
+		r->verdict = IXG_V_ICMP_ECHO;
+		r->l4_off = (uint16_t)l4;
+		r->l4_len = (uint16_t)l4len;
+		goto out;
+	}
+	set_drop(r, v6 ? IXG_V_DROP_IP6 : IXG_V_DROP_IP_PROTO); /* ip.c:106-107 */
+out:
+	if (csum)
+		*csum = (uint32_t)ip_res | ((uint32_t)l4_res << 16);
+}
+
+/* aux residual for ICMP is defined by reaching icmp's checksum step even
+ * when a NIC drop wins the verdict; recompute it here so the residual word
+ * does not depend on IXG_F_NO_CSUM_DROP */
+static void fix_icmp_residual(const uint8_t *frame, uint32_t L, uint32_t *csum)
+{
+	struct frame fr = {frame, L}, *f = &fr;
+	if (B16(f, 12) != 0x0800 || L < 34)
+		return;
+	uint32_t ver = B(f, 14) >> 4, ihl = B(f, 14) & 15, ip_len = B16(f, 16);
+	if (ver != 4 || ihl < 5 || (B16(f, 20) & 0x3FFF) || ip_len < ihl * 4 || 14 + ip_len > L ||
+	    B(f, 23) != 1)
+		return;
+	uint32_t l4len = ip_len - ihl * 4;
+	if (l4len < 8)
+		return;
+	uint16_t res = ixgo_chksum_internet(frame + 14 + ihl * 4, (int)l4len);
+	*csum = (*csum & 0xffffu) | ((uint32_t)res << 16);
+}
+
+void ixgo_rx_one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t len,
+		 struct ixg_rx_rec *rec, uint32_t *csum, int hash_mode, int work)
+{
+	static struct hashtab *ht_cache;
+	static uint8_t ht_key[IXG_RSS_KEY_LEN];
+	struct hashtab *ht = NULL;
+	if (hash_mode == IXGO_HASH_TABLE) {
+		if (!ht_cache) {
+			ht_cache = (struct hashtab *)malloc(sizeof(*ht_cache));
+			hashtab_build(ht_cache, cfg->rss_key);
+			memcpy(ht_key, cfg->rss_key, IXG_RSS_KEY_LEN);
+		} else if (memcmp(ht_key, cfg->rss_key, IXG_RSS_KEY_LEN)) {
+			hashtab_build(ht_cache, cfg->rss_key);
+			memcpy(ht_key, cfg->rss_key, IXG_RSS_KEY_LEN);
+		}
+		ht = ht_cache;
+	}
+	rx_one(cfg, ht, frame, len, rec, csum, work);
+	if (csum && work == IXGO_WORK_FULL)
+		fix_icmp_residual(frame, len, csum);
+}
+
+/* ---- batches ---------------------------------------------------------- */
+
+struct job {
+	const struct ixg_rx_cfg *cfg;
+	const struct hashtab *ht;
+	const uint8_t *base;
+	const uint64_t *off;
+	const uint16_t *len;
+	void *const *mbufs;
+	uint32_t stride, lo, hi;
+	struct ixg_rx_rec *out;
+	uint32_t *csum;
+	int work;
+};
+
+static void *run_job(void *arg)
+{
+	struct job *j = (struct job *)arg;
+	for (uint32_t i = j->lo; i < j->hi; i++) {
+		const uint8_t *fr;
+		uint32_t L;
+		if (j->mbufs) {
+			const uint8_t *m = (const uint8_t *)j->mbufs[i];
+			size_t l;
+			memcpy(&l, m, sizeof(l)); /* struct mbuf.len @0 (inc/ix/mbuf.h:73-74) */
+			fr = m + IXG_MBUF_HEADER_LEN;
+			L = (uint32_t)l;
+		} else {
+			fr = j->base + (j->off ? j->off[i] : (uint64_t)i * j->stride);
+			L = j->len[i];
+		}
+		uint32_t *c = j->csum ? &j->csum[i] : NULL;
+		rx_one(j->cfg, j->ht, fr, L, &j->out[i], c, j->work);
+		if (c && j->work == IXGO_WORK_FULL)
+			fix_icmp_residual(fr, L, c);
+	}
+	return NULL;
+}
+
+static int run_batch(struct job *proto, uint32_t n, int threads, int hash_mode)
+{
+	struct hashtab *ht = NULL;
+	if (hash_mode == IXGO_HASH_TABLE) {
+		ht = (struct hashtab *)malloc(sizeof(*ht));
+		if (!ht)
+			return -12;
+		hashtab_build(ht, proto->cfg->rss_key);
+	}
+	proto->ht = ht;
+	if (threads <= 1) {
+		proto->lo = 0;
+		proto->hi = n;
+		run_job(proto);
+	} else {
+		pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(*tid));
+		struct job *jobs = (struct job *)calloc((size_t)threads, sizeof(*jobs));
+		for (int t = 0; t < threads; t++) {
+			jobs[t] = *proto;
+			jobs[t].lo = (uint32_t)((uint64_t)n * t / threads);
+			jobs[t].hi = (uint32_t)((uint64_t)n * (t + 1) / threads);
+			pthread_create(&tid[t], NULL, run_job, &jobs[t]);
+		}
+		for (int t = 0; t < threads; t++)
+			pthread_join(tid[t], NULL);
+		free(tid);
+		free(jobs);
+	}
+	free(ht);
+	return 0;
+}
+
+int ixgo_rx_batch(const struct ixg_rx_cfg *cfg, const uint8_t *base, const uint64_t *off,
+		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out,
+		  uint32_t *csum, int threads, int hash_mode, int work)
+{
+	struct job j = {cfg, NULL, base, off, len, NULL, stride, 0, 0, out, csum, work};
+	return run_batch(&j, n, threads, hash_mode);
+}
+
+int ixgo_rx_batch_mbufs(const struct ixg_rx_cfg *cfg, void *const *mbufs, uint32_t n,
+			struct ixg_rx_rec *out, int threads, int hash_mode, int work)
+{
+	struct job j = {cfg, NULL, NULL, NULL, NULL, mbufs, 0, 0, 0, out, NULL, work};
+	return run_batch(&j, n, threads, hash_mode);
+}

@@ -1,0 +1,319 @@
+/*
+ * harness_main.c - drive the reference's own RX code over a frame file.
+ *
+ * TEST INFRASTRUCTURE ONLY (builds oracle/_ref/ixref_rx; used by
+ * tests/golden/make_golden.py to produce the committed golden vectors).
+ * No reference header is included here: every reference function is reached
+ * through the ref_* wrappers of the ref_*.c translation units.
+ *
+ * Per frame: the frame is placed in a zeroed IX mbuf (2112-B element, len at
+ * +0, data at +64: inc/ix/mbuf.h:73-90), the reference eth_input runs on it
+ * and the harness observes which callee it reached and with which L4
+ * pointer. Values come from the reference's functions: chksum_internet,
+ * inet_chksum_pseudo_partial, ip6_chksum_pseudo_partial, pbuf_header,
+ * tcp_to_idx, compute_toeplitz_hash. What the tree does not hold is restated
+ * here and flagged:
+ *   [NIC]  the driver's checksum/RSS applicability rules (DESIGN.md "NIC rules")
+ *   [UDP]  udp.c:59's length check (udp.c is unbuildable: needs Dune's mmu-x86.h)
+ *   [TCP]  the tcp_input head glue around pbuf_header (tcp_in.c:189,221-222,240)
+ *   [WHY]  drop reason codes; checked for consistency against the observed drop
+ *   [V6]   the IPv6 extension (reference drops 0x86DD); Toeplitz over 36 bytes
+ *          is compute_toeplitz_hash's loop generalised, parity unpinned
+ *
+ * Input file  (LE): "IXGRXIN1", u32 n, u32 cfg_flags, u16 nb_rx_fgs, u16 dev_idx,
+ *                   u8 key[40], u16 len[n], u32 off[n], u32 blob_len, blob.
+ * Output file (LE): "IXGRXOUT", u32 n, struct ixg_rx_rec[n] (16 B), u32 csum[n].
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ixgrx.h"
+#include "ref_capture.h"
+
+static void die(const char *m, uint32_t i)
+{
+	fprintf(stderr, "ixref_rx: %s (frame %u)\n", m, i);
+	exit(2);
+}
+
+static uint8_t Bz(const uint8_t *f, uint32_t L, uint32_t i) { return i < L ? f[i] : 0; }
+static uint16_t B16z(const uint8_t *f, uint32_t L, uint32_t i)
+{
+	return (uint16_t)((Bz(f, L, i) << 8) | Bz(f, L, i + 1));
+}
+static uint32_t raw32(const uint8_t *p)
+{
+	uint32_t v;
+	memcpy(&v, p, 4);
+	return v;
+}
+static uint16_t raw16(const uint8_t *p)
+{
+	uint16_t v;
+	memcpy(&v, p, 2);
+	return v;
+}
+
+/* [V6] bit-serial Toeplitz over n bytes, same loop as tcp_api.c:593-601 */
+static uint32_t toeplitz_n(const uint8_t *key, const uint8_t *in, int n)
+{
+	uint32_t r = 0, kp = ((uint32_t)key[0] << 24) | ((uint32_t)key[1] << 16) | ((uint32_t)key[2] << 8) | key[3];
+	for (int i = 0; i < n; i++)
+		for (int j = 128; j; j >>= 1) {
+			if (in[i] & j)
+				r ^= kp;
+			kp <<= 1;
+			if (key[i + 4] & j)
+				kp |= 1;
+		}
+	return r;
+}
+
+static void drop(struct ixg_rx_rec *r, uint8_t v)
+{
+	r->verdict = v;
+	r->l4_off = r->l4_len = 0;
+	r->pcb_bucket = IXG_NO_BUCKET;
+	r->tcp_flags = 0;
+}
+
+/* [WHY] the reason eth_input/ip_input/icmp_input dropped an IPv4/other frame */
+static uint8_t drop_reason(const uint8_t *f, uint32_t L)
+{
+	uint16_t et = B16z(f, L, 12);
+	if (et != 0x0800)
+		return IXG_V_DROP_ETHERTYPE;
+	uint32_t ver = Bz(f, L, 14) >> 4, ihl = Bz(f, L, 14) & 15, ip_len = B16z(f, L, 16);
+	if (L < 34) return IXG_V_DROP_IP_SHORT;
+	if (ver != 4) return IXG_V_DROP_IP_VERSION;
+	if (ihl < 5) return IXG_V_DROP_IP_IHL;
+	if (B16z(f, L, 20) & 0x3FFF) return IXG_V_DROP_IP_FRAG;
+	if (ip_len < ihl * 4) return IXG_V_DROP_IP_LEN;
+	if (14 + ip_len > L) return IXG_V_DROP_IP_TRUNC;
+	uint8_t proto = Bz(f, L, 23);
+	if (proto == 1) {
+		uint32_t l4 = 14 + ihl * 4, n = ip_len - ihl * 4;
+		if (n < 8) return IXG_V_DROP_ICMP_SHORT;
+		if (ref_chksum_internet(f + l4, (int)n)) return IXG_V_DROP_ICMP_CSUM;
+		return IXG_V_DROP_ICMP_TYPE;
+	}
+	return IXG_V_DROP_IP_PROTO;
+}
+
+static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, uint8_t *mbuf,
+		struct ixg_rx_rec *r, uint32_t *csum, uint32_t idx)
+{
+	uint8_t f[2048 + 64];
+	uint16_t ip_res = 0xffff, l4_res = 0xffff;
+	uint32_t rss = 0;
+	uint8_t flags = 0;
+
+	memset(r, 0, sizeof(*r));
+	r->pcb_bucket = IXG_NO_BUCKET;
+	memset(f, 0, sizeof(f));
+	memcpy(f, frame, L); /* a pristine copy: icmp_reflect rewrites the mbuf */
+
+	uint16_t et = B16z(f, L, 12);
+	uint32_t ver = f[14] >> 4, ihl = f[14] & 15, ip_len = B16z(f, L, 16), l4 = 14 + ihl * 4;
+	uint8_t proto = f[23];
+	int frag = (B16z(f, L, 20) & 0x3FFF) != 0;
+	int v6 = et == 0x86DD && (cfg->flags & IXG_F_IPV6);
+
+	/* [NIC] IP header checksum */
+	int hdr_ok = et == 0x0800 && ver == 4 && ihl >= 5 && l4 <= L;
+	if (hdr_ok) {
+		ip_res = ref_chksum_internet(f + 14, (int)(ihl * 4));
+		flags |= IXG_RF_IP_CSUM_CHECKED | (ip_res == 0 ? IXG_RF_IP_CSUM_OK : 0);
+	}
+	/* [NIC] RSS */
+	if (hdr_ok && !frag && (proto == 6 || proto == 17) && l4 + 4 <= L) {
+		rss = ref_toeplitz(cfg->rss_key, raw32(f + 26), raw32(f + 30), raw16(f + l4), raw16(f + l4 + 2));
+		flags |= IXG_RF_RSS;
+	} else if (v6 && L >= 58 && (f[14] >> 4) == 6 && (f[20] == 6 || f[20] == 17)) {
+		uint8_t in[36];
+		memcpy(in, f + 22, 32);
+		memcpy(in + 32, f + 54, 4);
+		rss = toeplitz_n(cfg->rss_key, in, 36);
+		flags |= IXG_RF_RSS;
+	}
+	r->rss_hash = rss;
+	r->fg_id = (uint16_t)(cfg->dev_idx * 512u + (rss & (uint32_t)(cfg->nb_rx_fgs - 1)));
+
+	/* [NIC] L4 checksum */
+	int l4c = 0;
+	if (hdr_ok && !frag && (proto == 6 || proto == 17) && ip_len >= ihl * 4 && 14 + ip_len <= L) {
+		uint32_t n = ip_len - ihl * 4;
+		if ((proto == 6 && n >= 20) || (proto == 17 && n >= 8 && B16z(f, L, l4 + 6) != 0)) {
+			l4_res = ref_pseudo_partial(f + l4, (uint16_t)n, proto, (uint16_t)n, raw32(f + 26), raw32(f + 30));
+			l4c = 1;
+		}
+	}
+	uint32_t plen = B16z(f, L, 18);
+	int v6ok = v6 && L >= 54 && (f[14] >> 4) == 6 && 54 + plen <= L;
+	if (v6ok && ((f[20] == 6 && plen >= 20) || (f[20] == 17 && plen >= 8))) {
+		l4_res = ref_pseudo6_partial(f + 54, (uint16_t)plen, f[20], (uint16_t)plen, f + 22, f + 38);
+		l4c = 1;
+	}
+	if (l4c)
+		flags |= IXG_RF_L4_CSUM_CHECKED | (l4_res == 0 ? IXG_RF_L4_CSUM_OK : 0);
+	r->flags = flags;
+
+	/* ICMP residual word: chksum_internet as icmp_input computes it */
+	if (et == 0x0800 && L >= 34 && ver == 4 && ihl >= 5 && !frag && ip_len >= ihl * 4 &&
+	    14 + ip_len <= L && proto == 1 && ip_len - ihl * 4 >= 8)
+		l4_res = ref_chksum_internet(f + l4, (int)(ip_len - ihl * 4));
+	*csum = (uint32_t)ip_res | ((uint32_t)l4_res << 16);
+
+	/* the driver drops on the NIC verdict (ixgbe.c:312-324,349) */
+	if (!(cfg->flags & IXG_F_NO_CSUM_DROP)) {
+		if ((flags & IXG_RF_IP_CSUM_CHECKED) && !(flags & IXG_RF_IP_CSUM_OK)) {
+			drop(r, IXG_V_DROP_CSUM_IP);
+			return;
+		}
+		if ((flags & IXG_RF_L4_CSUM_CHECKED) && !(flags & IXG_RF_L4_CSUM_OK)) {
+			drop(r, IXG_V_DROP_CSUM_L4);
+			return;
+		}
+	}
+
+	if (v6) {
+		/* [V6] extension; the reference eth_input drops this frame */
+		if (!v6ok || (f[20] != 6 && f[20] != 17)) {
+			drop(r, IXG_V_DROP_IP6);
+			return;
+		}
+		uint32_t n = plen;
+		if (f[20] == 6) {
+			if (n < 20) { drop(r, IXG_V_DROP_TCP_SHORT); return; }
+			uint8_t doff = f[54 + 12] >> 4;
+			uint16_t nl;
+			if (ref_pbuf_header_rom((uint16_t)n, (int16_t)-(doff * 4), &nl)) { drop(r, IXG_V_DROP_TCP_HDRLEN); return; }
+			r->verdict = IXG_V_TCP6;
+			r->l4_off = (uint16_t)(54 + doff * 4);
+			r->l4_len = nl;
+			r->tcp_flags = f[54 + 13] & 0x3f;
+		} else {
+			uint16_t ulen = B16z(f, L, 54 + 4);
+			if (54 + ulen > L) { drop(r, IXG_V_DROP_UDP_LEN); return; }
+			r->verdict = IXG_V_UDP6;
+			r->l4_off = 54 + 8;
+			r->l4_len = ulen;
+		}
+		return;
+	}
+
+	/* the reference eth_input, for real */
+	size_t len = L;
+	memset(mbuf, 0, IXG_MBUF_STRIDE);
+	memcpy(mbuf, &len, sizeof(len));
+	memcpy(mbuf + IXG_MBUF_HEADER_LEN, f, L);
+	ref_eth_input(mbuf);
+
+	switch (ref_cap.kind) {
+	case REF_NONE: {
+		if (!ref_cap.freed)
+			die("eth_input neither delivered nor freed", idx);
+		uint8_t why = drop_reason(f, L);
+		drop(r, why);
+		return;
+	}
+	case REF_TCP: {
+		if (ref_cap.freed)
+			die("tcp delivered and freed", idx);
+		uint32_t off = (uint32_t)ref_cap.l4_off;
+		uint16_t n = ref_cap.l4_len;
+		if (off != l4)
+			die("tcp l4 offset mismatch", idx);
+		/* [TCP] tcp_input head (tcp_in.c:189,221-222) */
+		if (n < 20) { drop(r, IXG_V_DROP_TCP_SHORT); return; }
+		uint8_t doff = f[off + 12] >> 4; /* TCPH_HDRLEN */
+		uint16_t nl;
+		if (ref_pbuf_header_rom(n, (int16_t)-(doff * 4), &nl)) { drop(r, IXG_V_DROP_TCP_HDRLEN); return; }
+		r->verdict = IXG_V_TCP;
+		r->l4_off = (uint16_t)(off + doff * 4);
+		r->l4_len = nl;
+		r->tcp_flags = f[off + 13] & 0x3f;
+		/* tcp_in.c:230-233: ports to host order, local = dst, remote = src */
+		r->pcb_bucket = (uint16_t)ref_tcp_to_idx(raw32(f + 30), raw32(f + 26),
+							 (uint16_t)((f[off + 2] << 8) | f[off + 3]),
+							 (uint16_t)((f[off] << 8) | f[off + 1]));
+		return;
+	}
+	case REF_UDP: {
+		if (ref_cap.freed)
+			die("udp delivered and freed", idx);
+		uint32_t off = (uint32_t)ref_cap.l4_off;
+		uint16_t ulen = B16z(f, L, off + 4);
+		/* [UDP] mbuf_enough_space(pkt, udphdr, len) (udp.c:59) */
+		if (off + (uint32_t)ulen > L) { drop(r, IXG_V_DROP_UDP_LEN); return; }
+		r->verdict = IXG_V_UDP;
+		r->l4_off = (uint16_t)(off + 8);
+		r->l4_len = ulen;
+		return;
+	}
+	case REF_ARP:
+		r->verdict = IXG_V_ARP;
+		r->l4_off = (uint16_t)ref_cap.l4_off;
+		r->l4_len = (uint16_t)(L >= 14 ? L - 14 : 0);
+		return;
+	case REF_ICMP_REFLECT:
+		r->verdict = IXG_V_ICMP_ECHO;
+		r->l4_off = (uint16_t)l4;
+		r->l4_len = (uint16_t)(ip_len - ihl * 4);
+		return;
+	}
+	die("unknown capture", idx);
+}
+
+int main(int argc, char **argv)
+{
+	if (argc != 3) {
+		fprintf(stderr, "usage: ixref_rx IN OUT\n");
+		return 1;
+	}
+	FILE *fi = fopen(argv[1], "rb");
+	if (!fi)
+		die("open input", 0);
+	char magic[8];
+	uint32_t n, cflags, blob_len;
+	uint16_t nb, dev;
+	struct ixg_rx_cfg cfg;
+	if (fread(magic, 1, 8, fi) != 8 || memcmp(magic, "IXGRXIN1", 8))
+		die("bad magic", 0);
+	if (fread(&n, 4, 1, fi) != 1 || fread(&cflags, 4, 1, fi) != 1 || fread(&nb, 2, 1, fi) != 1 ||
+	    fread(&dev, 2, 1, fi) != 1 || fread(cfg.rss_key, 1, 40, fi) != 40)
+		die("short header", 0);
+	cfg.flags = cflags;
+	cfg.nb_rx_fgs = nb;
+	cfg.dev_idx = dev;
+	uint16_t *len = malloc(sizeof(uint16_t) * (n + 1));
+	uint32_t *off = malloc(sizeof(uint32_t) * (n + 1));
+	if (fread(len, 2, n, fi) != n || fread(off, 4, n, fi) != n || fread(&blob_len, 4, 1, fi) != 1)
+		die("short arrays", 0);
+	uint8_t *blob = malloc(blob_len + 1);
+	if (fread(blob, 1, blob_len, fi) != blob_len)
+		die("short blob", 0);
+	fclose(fi);
+
+	if (ref_ix_init())
+		die("arch_prctl(ARCH_SET_GS)", 0);
+	uint8_t *mbuf = aligned_alloc(64, IXG_MBUF_STRIDE);
+	struct ixg_rx_rec *recs = calloc(n + 1, sizeof(*recs));
+	uint32_t *cs = calloc(n + 1, sizeof(*cs));
+	for (uint32_t i = 0; i < n; i++) {
+		if (len[i] > IXG_MBUF_DATA_LEN || (uint64_t)off[i] + len[i] > blob_len)
+			die("frame does not fit an mbuf", i);
+		one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], i);
+	}
+	FILE *fo = fopen(argv[2], "wb");
+	if (!fo)
+		die("open output", 0);
+	fwrite("IXGRXOUT", 1, 8, fo);
+	fwrite(&n, 4, 1, fo);
+	fwrite(recs, sizeof(*recs), n, fo);
+	fwrite(cs, 4, n, fo);
+	fclose(fo);
+	return 0;
+}

@@ -1,0 +1,29 @@
+/* ref_capture.h - what the reference harness observes (test infrastructure). */
+#ifndef REF_CAPTURE_H
+#define REF_CAPTURE_H
+#include <stdint.h>
+
+enum { REF_NONE = 0, REF_TCP, REF_UDP, REF_ARP, REF_ICMP_REFLECT };
+
+struct ref_capture {
+	int kind;        /* which callee eth_input reached (REF_NONE: none) */
+	long l4_off;     /* L4 header pointer - frame start, as passed to the callee */
+	uint16_t l4_len; /* tcp_input_tmp's pbuf length */
+	int freed;       /* mbuf_free reached mempool_free_2 (= dropped) */
+};
+
+extern struct ref_capture ref_cap;
+
+int ref_ix_init(void);
+void ref_eth_input(void *mbuf);
+uint16_t ref_chksum_internet(const void *buf, int len);
+
+uint16_t ref_pseudo_partial(const void *seg, uint16_t len, uint8_t proto, uint16_t proto_len,
+			    uint32_t src_raw, uint32_t dst_raw);
+uint16_t ref_pseudo6_partial(const void *seg, uint16_t len, uint8_t proto, uint16_t proto_len,
+			     const void *src16, const void *dst16);
+int ref_pbuf_header_rom(uint16_t len, int16_t inc, uint16_t *new_len);
+int ref_tcp_to_idx(uint32_t local_raw, uint32_t remote_raw, uint16_t local_port, uint16_t remote_port);
+uint32_t ref_toeplitz(const uint8_t *key, uint32_t src_raw, uint32_t dst_raw, uint16_t sport_raw,
+		      uint16_t dport_raw);
+#endif
