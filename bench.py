@@ -210,11 +210,15 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
     key = traces.RSS_KEY
-    eng = ixgrx.RxEngine(ixgrx.Config(key, 128, rank % 128, 0), device=local)
-    eng2 = None
+    engs = {}
+
+    def engine(flags):
+        if flags not in engs:
+            engs[flags] = ixgrx.RxEngine(ixgrx.Config(key, 128, rank % 128, flags), device=local)
+        return engs[flags]
 
     wl = Workload(args.workload, seed=0x1B0000 + 2 + 97 * rank, dev=dev, n=args.n)
-    el, kavg, kmin = time_steps(wl, eng, args.steps, args.warmup, dist, world)
+    el, kavg, kmin = time_steps(wl, engine(wl.flags), args.steps, args.warmup, dist, world)
     ok = wl.check(key) if rank == 0 else True
     primary = (wl.name, wl.pool, wl.flags)
     total = wl.n * args.steps * world
@@ -250,7 +254,7 @@ def main():
         del wl
         torch.cuda.empty_cache()
         wl2 = Workload(args.secondary, seed=0x1B0000 + 4 + 97 * rank, dev=dev)
-        el2, k2, _ = time_steps(wl2, eng, max(5, args.steps // 2), 2, dist, world)
+        el2, k2, _ = time_steps(wl2, engine(wl2.flags), max(5, args.steps // 2), 2, dist, world)
         ok2 = wl2.check(key) if rank == 0 else True
         m2 = wl2.n * max(5, args.steps // 2) * world / el2 / 1e6
         a2 = wl2.bytes_per_pkt * wl2.n / k2 / 1e9
@@ -264,7 +268,7 @@ def main():
         del wl
         torch.cuda.empty_cache()
         wlc = Workload(args.workload, seed=0x1B0000 + 2, dev=dev, n=args.n)
-        res["copy_inclusive"] = copy_inclusive(wlc, eng, key)
+        res["copy_inclusive"] = copy_inclusive(wlc, engine(wlc.flags), key)
         del wlc
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
@@ -279,9 +283,8 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    eng.close()
-    if eng2:
-        eng2.close()
+    for e in engs.values():
+        e.close()
 
 
 if __name__ == "__main__":

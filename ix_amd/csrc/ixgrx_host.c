@@ -19,7 +19,12 @@ struct ixg_ctx {
 	int device;
 	struct ixg_rx_cfg cfg;
 	uint32_t crc_const;
-	uint32_t grid_max;
+	uint32_t grid_fast;  /* persistent grids: CUs x resident blocks per CU */
+	uint32_t grid_gen;
+	int force_general;   /* IXGRX_FORCE_GENERAL=1: skip the fixed-shape kernel (tests/A-B) */
+	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
+	uint8_t *d_defer;    /* one flag per 64-packet chunk */
+	size_t defer_cap;
 	uint64_t *d_tab;
 	uint32_t *d_tab6;
 	hipStream_t stream; /* for the synchronous host paths */
@@ -136,6 +141,7 @@ void ixg_rx_fini(void *vctx)
 		hipStreamSynchronize(c->stream);
 	hipFree(c->d_tab);
 	hipFree(c->d_tab6);
+	hipFree(c->d_defer);
 	hipFree(c->d_frames);
 	hipFree(c->d_off);
 	hipFree(c->d_len);
@@ -175,7 +181,16 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 	hipDeviceProp_t prop;
 	if (hipGetDeviceProperties(&prop, device) != hipSuccess)
 		goto fail;
-	c->grid_max = (uint32_t)prop.multiProcessorCount * (uint32_t)ixgrx_blocks_per_cu();
+	{
+		const char *e = getenv("IXGRX_FORCE_GENERAL");
+		c->force_general = e && e[0] == '1';
+		e = getenv("IXGRX_FAST_VARIANT");
+		c->fast_variant = e ? (atoi(e) & 0xff) : 0;
+		e = getenv("IXGRX_GEN_VARIANT");
+		c->fast_variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
+	}
+	c->grid_fast = (uint32_t)prop.multiProcessorCount * (uint32_t)ixgrx_blocks_per_cu(c->fast_variant & 0xff);
+	c->grid_gen = (uint32_t)prop.multiProcessorCount * (uint32_t)ixgrx_blocks_per_cu(-1 - ((c->fast_variant >> 8) & 0xff));
 	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
 	if (!tab) {
 		rc = -ENOMEM;
@@ -231,12 +246,29 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 	p.flags = c->cfg.flags;
 	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
 	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
+	size_t nchunks = ((size_t)n + 63) / 64;
+	if (!c->force_general) {
+		if (nchunks > c->defer_cap) {
+			/* grows once per larger batch; not inside a graph capture */
+			hipFree(c->d_defer);
+			c->d_defer = NULL;
+			c->defer_cap = 0;
+			size_t cap = nchunks + nchunks / 4 + 64;
+			HIPCHK(hipMalloc((void **)&c->d_defer, cap));
+			c->defer_cap = cap;
+		}
+		p.defer = c->d_defer;
+	}
 	uint32_t blk = ixgrx_block();
-	uint64_t want = ((uint64_t)n + blk - 1) / blk;
-	uint32_t grid = want < c->grid_max ? (uint32_t)want : c->grid_max;
-	if (grid == 0)
-		grid = 1;
-	return ixgrx_launch(&p, grid, s) == 0 ? 0 : -EIO;
+	uint64_t want_f = (nchunks + blk / 64 - 1) / (blk / 64);     /* one wave per chunk */
+	uint64_t want_g = (nchunks + 255) / 256;                          /* one workgroup per 256 chunks */
+	uint32_t gf = want_f < c->grid_fast ? (uint32_t)want_f : c->grid_fast;
+	uint32_t gg = want_g < c->grid_gen ? (uint32_t)want_g : c->grid_gen;
+	if (gf == 0)
+		gf = 1;
+	if (gg == 0)
+		gg = 1;
+	return ixgrx_launch(&p, c->fast_variant, gf, gg, s) == 0 ? 0 : -EIO;
 }
 
 int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,

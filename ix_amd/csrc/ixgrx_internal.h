@@ -26,14 +26,16 @@ struct ixg_kparams {
 	uint32_t flags;
 	uint32_t fg_base;      /* dev_idx * 512 */
 	uint32_t fg_mask;      /* nb_rx_fgs - 1 */
+	uint8_t *defer;        /* per 64-packet chunk: 1 = left for the general
+	                          kernel; NULL = general kernel does everything */
 };
 typedef struct ixg_kparams ixg_kparams;
 
 /* implemented in ixgrx_kernels.hip */
-int ixgrx_launch(const void *params, uint32_t grid, void *stream);
+int ixgrx_launch(const void *params, int fast_variant, uint32_t grid_fast, uint32_t grid_gen, void *stream);
 uint32_t ixgrx_kparams_size(void);
 uint32_t ixgrx_block(void);
-int ixgrx_blocks_per_cu(void);
+int ixgrx_blocks_per_cu(int which); /* >= 0: fixed-shape kernel variant k, < 0: general variant -1-which */
 
 #ifdef __cplusplus
 }

@@ -101,6 +101,17 @@ DEV uint64_t region_sum(const uint32_t (&d)[N], int qa, int e) {
   return s;
 }
 
+// 16-byte load that is always issued: lanes that must not read their
+// frame read `dummy` (an always-valid L1-resident address). Every consumer
+// masks by the frame/segment length, so the dummy bytes never count, and
+// no select touches the value at issue time (that would force an immediate
+// vmcnt wait). Loads inside exec-masked branches make hipcc count them as
+// possibly not issued, so its vmcnt waits for the current data would also
+// wait for the loads prefetched for the next step.
+DEV u32x4 load16(bool ok, const uint8_t* addr, const uint8_t* dummy) {
+  return *reinterpret_cast<const u32x4_a4*>(ok ? addr : dummy);
+}
+
 struct Rec {
   uint32_t w0, w1, w2, w3;  // the 16-byte ixg_rx_rec as four dwords
 };
@@ -258,8 +269,12 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   if (FAST) s.stream = false;
 }
 
-// Verdict + record once the L4 sum is complete (mirrors ixgo rx_one order).
-DEV void lane_finish(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t L, LaneState& s) {
+// The record for a lane given its L4 residual: the residual computed, or a
+// hypothesis (0 / non-zero) for a long segment whose tail is summed later.
+// Mirrors the verdict order of the oracle's rx_one (driver checksum drops,
+// then eth_input / ip_input / tcp_input head / udp_input / icmp_input).
+DEV Rec make_record(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t L, const LaneState& s,
+                    uint32_t l4_res) {
   const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
   const uint32_t vh = byte_at(d, 14);
   const uint32_t ver = vh >> 4, ihl = vh & 15u;
@@ -267,19 +282,15 @@ DEV void lane_finish(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t 
   const uint32_t ip_off = (byte_at(d, 20) << 8) | byte_at(d, 21);
   const bool frag = (ip_off & 0x3fffu) != 0;
 
-  s.l4_res = 0xffffu;
-  if (s.l4_kind) {
-    s.l4_res = (~fold16(s.l4_acc)) & 0xffffu;
-    if (s.l4_kind == 1)
-      s.flags |= IXG_RF_L4_CSUM_CHECKED | (s.l4_res == 0 ? IXG_RF_L4_CSUM_OK : 0u);
-  }
+  uint32_t flags = s.flags;
+  if (s.l4_kind == 1) flags |= IXG_RF_L4_CSUM_CHECKED | (l4_res == 0 ? IXG_RF_L4_CSUM_OK : 0u);
 
   uint32_t v = 0, off = 0, len = 0, bucket = IXG_NO_BUCKET, tfl = 0;
   const bool csum_drop = !(p.flags & IXG_F_NO_CSUM_DROP);
   const uint32_t proto = s.proto, l4 = s.l4, l4len = s.l4len;
-  if (csum_drop && (s.flags & IXG_RF_IP_CSUM_CHECKED) && !(s.flags & IXG_RF_IP_CSUM_OK)) {
+  if (csum_drop && (flags & IXG_RF_IP_CSUM_CHECKED) && !(flags & IXG_RF_IP_CSUM_OK)) {
     v = IXG_V_DROP_CSUM_IP;                                         // ixgbe.c:313-317
-  } else if (csum_drop && (s.flags & IXG_RF_L4_CSUM_CHECKED) && !(s.flags & IXG_RF_L4_CSUM_OK)) {
+  } else if (csum_drop && (flags & IXG_RF_L4_CSUM_CHECKED) && !(flags & IXG_RF_L4_CSUM_OK)) {
     v = IXG_V_DROP_CSUM_L4;                                         // ixgbe.c:320-324
   } else if (etype == 0x0806u) {                                    // ip.c:134-135
     v = IXG_V_ARP; off = 14; len = L >= 14 ? L - 14 : 0;
@@ -325,7 +336,7 @@ DEV void lane_finish(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t 
         }
       } else if (proto == 1 && !s.v6) {
         if (l4len < 8) v = IXG_V_DROP_ICMP_SHORT;                   // icmp.c:80
-        else if (s.l4_res != 0) v = IXG_V_DROP_ICMP_CSUM;           // icmp.c:82
+        else if (l4_res != 0) v = IXG_V_DROP_ICMP_CSUM;             // icmp.c:82
         else if (s.icmp_type != 8) v = IXG_V_DROP_ICMP_TYPE;        // icmp.c:88-108
         else { v = IXG_V_ICMP_ECHO; off = l4; len = l4len; }
       } else {
@@ -333,24 +344,41 @@ DEV void lane_finish(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t 
       }
     }
   }
-  s.verdict = v;
-  s.l4_off = off & 0xffffu;
-  s.l4_len = len & 0xffffu;
-  s.bucket = bucket;
-  s.tcp_flags = tfl;
+  Rec r;
+  r.w0 = (s.fg & 0xffffu) | (v << 16) | (flags << 24);
+  r.w1 = (off & 0xffffu) | ((len & 0xffffu) << 16);
+  r.w2 = s.rss;
+  r.w3 = bucket | (tfl << 16);
+  return r;
 }
 
-DEV const uint8_t* frame_ptr(const KParams& p, uint32_t i) {
-  return p.base + (p.off ? p.off[i] : (uint64_t)i * p.stride);
+DEV uint32_t l4_residual(const LaneState& s) { return s.l4_kind ? ((~fold16(s.l4_acc)) & 0xffffu) : 0xffffu; }
+
+DEV void store_record(const KParams& p, uint32_t i, const Rec& r, uint32_t ip_res, uint32_t l4_res) {
+  u32x4 w = {r.w0, r.w1, r.w2, r.w3};
+  *reinterpret_cast<u32x4*>(p.out + i) = w;
+  if (p.csum) p.csum[i] = ip_res | (l4_res << 16);
+}
+
+// Frame i's byte offset. The layout (u64 offsets vs fixed stride) is a
+// template parameter, not a runtime branch: a branch on p.off makes hipcc
+// join the two paths with a conservative s_waitcnt vmcnt(0) that drains
+// every load in flight (and with it any software pipelining).
+template <bool OFFS>
+DEV uint64_t frame_off(const KParams& p, uint32_t i) {
+  return OFFS ? p.off[i] : (uint64_t)i * p.stride;
 }
 
 // load 16-byte chunks [K0, K1) of the prefix; chunk k only if 16k < L
 template <int K0, int K1>
-DEV void load_prefix(const uint8_t* f, uint32_t L, uint32_t (&d)[kPrefixDw]) {
+DEV void load_prefix(const uint8_t* f, uint32_t L, const uint8_t* dummy, uint32_t (&d)[kPrefixDw]) {
+  static_assert(K0 == 0, "prefix loads start at the frame start");
+  // bytes 0..11 (MAC addresses) are never read: one dword for 12..15
+  d[0] = d[1] = d[2] = 0;
+  d[3] = *reinterpret_cast<const uint32_t*>((12u < L ? f : dummy) + 12) & ones((int)L - 12 < 0 ? 0 : (int)L - 12);
 #pragma unroll
-  for (int k = K0; k < K1; k++) {
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if ((uint32_t)(16 * k) < L) v = *reinterpret_cast<const u32x4_a4*>(f + 16 * k);
+  for (int k = K0 + 1; k < K1; k++) {
+    const u32x4 v = load16((uint32_t)(16 * k) < L, f + 16 * k, dummy);
     // bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L")
     d[4 * k + 0] = v.x & ones((int)L - (16 * k + 0) < 0 ? 0 : (int)L - (16 * k + 0));
     d[4 * k + 1] = v.y & ones((int)L - (16 * k + 4) < 0 ? 0 : (int)L - (16 * k + 4));
@@ -359,127 +387,378 @@ DEV void load_prefix(const uint8_t* f, uint32_t L, uint32_t (&d)[kPrefixDw]) {
   }
 }
 
-// Cooperative sum of [kStreamBase, seg_end) for the lanes with s.stream set.
-DEV void stream_sums(const KParams& p, uint32_t pkt0, int lane, uint32_t* lds_list, uint32_t* lds_sum,
-                     LaneState& s) {
-  const uint64_t lm = __ballot(s.stream);
-  if (lm == 0) return;
-  const int nlong = __popcll(lm);
-  // wave compaction: rank of this lane among the long lanes
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(lm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lm, 0u));
-  if (s.stream) lds_list[rank] = (uint32_t)lane;
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  const int grp = lane / kGroup, gl = lane % kGroup;
-  const uint32_t my_end = s.seg_end;
-  for (int r0 = 0; r0 < nlong; r0 += 64 / kGroup) {
-    const int k = r0 + grp;
-    const bool act = k < nlong;
-    const uint32_t owner = act ? lds_list[k] : 0u;
-    const uint32_t end = (uint32_t)__shfl((int)my_end, (int)owner);
-    const uint8_t* f = frame_ptr(p, pkt0 + owner);
-    uint64_t acc = 0;
-    // chunk c covers bytes [96 + 16c, 96 + 16c + 16); lane gl takes c = gl + 16t
-    for (uint32_t c0 = 0;; c0 += kGroup * kStreamUnroll) {
-      const bool more = act && (uint32_t)kStreamBase + 16u * c0 < end;
-      if (!__any(more)) break;
-      u32x4 v[kStreamUnroll];
+
+// the fixed-shape path: everything in the 64-byte prefix
+DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, bool valid, uint32_t L,
+                      const uint32_t (&d)[kPrefixDw]) {
+  LaneState s;
+  lane_parse<true>(p, T, d, L, s);
+  if (valid) {
+    const uint32_t r4 = l4_residual(s);
+    store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
+  }
+}
+
+// ---- general path: pass A (lane per packet, 96-byte prefix) + pass B
+// (segments past the prefix, compacted into a per-workgroup LDS list and
+// streamed lane-per-packet with U 16-byte loads in flight per lane).
+constexpr int kLongCap = 512;  // list capacity; flushed at >= 256 entries
+
+// LDS (address space 3) pointers: through generic pointers these would be
+// flat_* accesses, which count on vmcnt as well and force vmcnt(0) waits
+// that serialise the streaming loads.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+#define LDS(T, x) ((T*)(x))
+
+struct LongList {
+  lds_u32* cnt;
+  lds_u32* pkt;     // packet index
+  lds_u32* end;     // segment end (frame offset)
+  lds_u32* acc;     // folded sum of the in-prefix part + pseudo header
+  lds_u32* ipres;   // IP header residual (csum output)
+  lds_u32x4* rec_ok;   // record if the L4 residual is 0
+  lds_u32x4* rec_bad;  // record if it is not
+};
+
+template <bool OFFS>
+DEV void pass_a_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
+                      const LongList& ll) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t ic = valid ? i : p.n - 1;  // clamped: descriptor loads without a branch
+  const uint32_t L = valid ? (uint32_t)p.len[ic] : 0u;
+  const uint8_t* f = p.base + frame_off<OFFS>(p, ic);
+  uint32_t d[kPrefixDw];
+  load_prefix<0, 6>(f, L, reinterpret_cast<const uint8_t*>(p.tab), d);
+  LaneState s;
+  lane_parse<false>(p, T, d, L, s);
+  const bool lng = valid && s.stream;
+  const uint64_t m = __ballot(lng);
+  if (m) {
+    uint32_t base = 0;
+    if (lane == 0) base = __hip_atomic_fetch_add(ll.cnt, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    base = (uint32_t)__shfl((int)base, 0);
+    if (lng) {
+      const uint32_t e = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      ll.pkt[e] = i;
+      ll.end[e] = s.seg_end;
+      ll.acc[e] = fold32(s.l4_acc);
+      ll.ipres[e] = s.ip_res;
+      const Rec ok = make_record(p, d, L, s, 0u), bad = make_record(p, d, L, s, 1u);
+      ll.rec_ok[e] = u32x4{ok.w0, ok.w1, ok.w2, ok.w3};
+      ll.rec_bad[e] = u32x4{bad.w0, bad.w1, bad.w2, bad.w3};
+    }
+  }
+  if (valid && !lng) {
+    const uint32_t r4 = l4_residual(s);
+    store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
+  }
+}
+
+// end-around sum over the whole wave (every lane gets the total)
+DEV uint32_t wave_sum1c(uint32_t a) {
 #pragma unroll
-      for (int t = 0; t < kStreamUnroll; t++) {
-        const uint32_t pos = kStreamBase + 16u * (c0 + gl + kGroup * t);
-        v[t] = u32x4{0u, 0u, 0u, 0u};
-        if (act && pos < end) v[t] = *reinterpret_cast<const u32x4_a4*>(f + pos);
-      }
+  for (int m = 1; m < 64; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, 64));
+  return a;
+}
+
+// masked sum of a 16-byte piece whose first byte is `rem` bytes before the
+// segment end (rem <= 0: nothing of it is inside)
+DEV uint64_t piece_sum(const u32x4& v, int rem) {
+  return (uint64_t)(v.x & ones(rem < 0 ? 0 : rem)) + (v.y & ones(rem - 4 < 0 ? 0 : rem - 4)) +
+         (v.z & ones(rem - 8 < 0 ? 0 : rem - 8)) + (v.w & ones(rem - 12 < 0 ? 0 : rem - 12));
+}
+
+// Pass B: one wave per packet, its segment tail [96, end) read as fully
+// coalesced 1 KiB wave-instructions; the loads of P packets are issued
+// before the first reduction. Entries are dealt to waves round-robin.
+template <bool OFFS, int P>
+DEV void pass_b(const KParams& p, uint32_t cnt, const LongList& ll) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int kPiece = 2;  // 2 KiB per packet per pass: frames up to 2144 B in one pass
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.tab) + 16 * lane;
+  for (uint32_t k0 = (uint32_t)wave; k0 < cnt; k0 += kWaves * P) {
+    uint32_t ends[P];
+    uint64_t offs[P];
 #pragma unroll
-      for (int t = 0; t < kStreamUnroll; t++) {
-        const uint32_t pos = kStreamBase + 16u * (c0 + gl + kGroup * t);
-        const int rem = (int)end - (int)pos;  // bytes of this chunk inside the segment
-        acc += v[t].x & ones(rem < 0 ? 0 : rem);
-        acc += v[t].y & ones(rem - 4 < 0 ? 0 : rem - 4);
-        acc += v[t].z & ones(rem - 8 < 0 ? 0 : rem - 8);
-        acc += v[t].w & ones(rem - 12 < 0 ? 0 : rem - 12);
+    for (int j = 0; j < P; j++) {  // addresses first (uniform: LDS broadcast + scalar loads)
+      const uint32_t e = k0 + (uint32_t)(kWaves * j);
+      const uint32_t ec = e < cnt ? e : 0u;
+      ends[j] = e < cnt ? ll.end[ec] : 0u;
+      const uint32_t pk = __builtin_amdgcn_readfirstlane(ll.pkt[ec]);
+      offs[j] = frame_off<OFFS>(p, pk);
+    }
+    u32x4 v[P][kPiece];
+#pragma unroll
+    for (int j = 0; j < P; j++) {  // then every packet's loads, back to back
+#pragma unroll
+      for (int t = 0; t < kPiece; t++) {
+        const uint32_t pos = kStreamBase + 16u * lane + 1024u * t;
+        v[j][t] = load16(pos < ends[j], p.base + offs[j] + pos, dummy);
       }
     }
-    uint32_t a = fold32(acc);
+    uint32_t part[P];
 #pragma unroll
-    for (int m = 1; m < kGroup; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, kGroup));
-    if (act && gl == 0) lds_sum[owner] = a;
+    for (int j = 0; j < P; j++) {
+      uint64_t acc = 0;
+#pragma unroll
+      for (int t = 0; t < kPiece; t++)
+        acc += piece_sum(v[j][t], (int)ends[j] - (int)(kStreamBase + 16u * lane + 1024u * t));
+      part[j] = fold32(acc);
+    }
+    // frames longer than 96 + 2 KiB (not IX mbufs, whose data is <= 2048 B):
+    // the rest, one KiB at a time, after the batch so the common path keeps
+    // all P packets' loads in flight together
+    uint32_t emax = 0;
+#pragma unroll
+    for (int j = 0; j < P; j++) emax = ends[j] > emax ? ends[j] : emax;
+    if (emax > kStreamBase + 1024u * kPiece) {
+#pragma unroll
+      for (int j = 0; j < P; j++) {
+        for (uint32_t pos0 = kStreamBase + 1024u * kPiece; pos0 < ends[j]; pos0 += 1024u) {
+          const uint32_t pos = pos0 + 16u * lane;
+          const u32x4 w = load16(pos < ends[j], p.base + offs[j] + pos, dummy);
+          part[j] = add1c(part[j], fold32(piece_sum(w, (int)ends[j] - (int)pos)));
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < P; j++) {
+      const uint32_t e = k0 + (uint32_t)(kWaves * j);
+      const uint32_t tot = wave_sum1c(part[j]);
+      if (lane == 0 && e < cnt) {
+        const uint32_t res = (~fold16(add1c(ll.acc[e], tot))) & 0xffffu;
+        const uint32_t i = ll.pkt[e];
+        *reinterpret_cast<u32x4*>(p.out + i) = res == 0 ? ll.rec_ok[e] : ll.rec_bad[e];
+        if (p.csum) p.csum[i] = ll.ipres[e] | (res << 16);
+      }
+    }
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  if (s.stream) s.l4_acc += lds_sum[lane];
 }
 
-template <bool FAST>
-DEV void process(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, bool valid, uint32_t L,
-                 uint32_t (&d)[kPrefixDw], uint32_t pkt0, int lane, uint32_t* lds_list, uint32_t* lds_sum) {
-  LaneState s;
-  lane_parse<FAST>(p, T, d, L, s);
-  if (!FAST) {
-    if (!valid) s.stream = false;
-    stream_sums(p, pkt0, lane, lds_list, lds_sum, s);
-  }
-  lane_finish(p, d, L, s);
-  if (valid) {
-    Rec r;
-    r.w0 = (s.fg & 0xffffu) | (s.verdict << 16) | (s.flags << 24);
-    r.w1 = s.l4_off | (s.l4_len << 16);
-    r.w2 = s.rss;
-    r.w3 = s.bucket | (s.tcp_flags << 16);
-    u32x4 w = {r.w0, r.w1, r.w2, r.w3};
-    *reinterpret_cast<u32x4*>(p.out + i) = w;
-    if (p.csum) p.csum[i] = s.ip_res | (s.l4_res << 16);
-  }
-}
-
-}  // namespace
-
-extern "C" __global__ void __launch_bounds__(kBlock)
-ixg_rx_kernel(KParams p) {
-  __shared__ uint64_t T[12 * 256];
-  __shared__ uint32_t lds_list[kWaves][64];
-  __shared__ uint32_t lds_sum[kWaves][64];
-  // stage the hash tables (24 KiB) once per persistent workgroup
+// stage the hash tables (24 KiB) once per persistent workgroup
+DEV void stage_tables(const KParams& p, uint64_t* T) {
   for (int k = threadIdx.x; k < 12 * 256 / 2; k += kBlock) {
     const u32x4 v = reinterpret_cast<const u32x4*>(p.tab)[k];
     reinterpret_cast<u32x4*>(T)[k] = v;
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (uint32_t blk = blockIdx.x * kBlock; blk < p.n; blk += gridDim.x * kBlock) {
-    const uint32_t pkt0 = blk + wave * 64;
-    const uint32_t i = pkt0 + lane;
-    const bool valid = i < p.n;
-    const uint32_t L = valid ? p.len[i] : 0u;
-    const uint8_t* f = valid ? frame_ptr(p, i) : p.base;
-    uint32_t d[kPrefixDw];
-    load_prefix<0, 4>(f, L, d);
+}
+
+// ---- fixed-shape kernel --------------------------------------------------
+// Software-pipelined over the wave's chunks (64 packets each, grid-stride):
+// descriptors (len, offset) are fetched two chunks ahead, the 64-byte
+// prefixes one chunk ahead, so a wave always has its next chunk's frame
+// bytes in flight while it computes the current one. Chunks that are not
+// all "fast shape" are flagged for the general kernel.
+
+template <bool OFFS>
+DEV void fetch_desc(const KParams& p, uint32_t chunk, int lane, uint32_t& L, uint64_t& o) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const uint32_t ic = i < p.n ? i : p.n - 1;  // clamped, branch-free
+  L = p.len[ic];
+  o = frame_off<OFFS>(p, ic);
+}
+
+// The fast path never reads bytes 0..11 (MAC addresses): load exactly
+// bytes 12..63 (one dword + three 16-byte loads). Loading 0..15 as one
+// dwordx4 leaves dead lanes in the destination that the register allocator
+// reuses at once, and that write-after-write forces a vmcnt(0) right after
+// the prefetch is issued.
+struct Prefix {
+  uint32_t w3;   // bytes 12..15
+  u32x4 v[3];    // bytes 16..63
+};
+
+DEV void fetch_prefix(const KParams& p, uint32_t chunk, int lane, uint32_t L, uint64_t o, Prefix& x) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  // only frames that can be fast are worth loading; the bytes may run past
+  // L into the next frame or the tail pad (include/ixgrx.h IXG_TAIL_PAD)
+  const bool ok = i < p.n && L <= 64u;
+  const uint8_t* f = ok ? p.base + o : reinterpret_cast<const uint8_t*>(p.tab);
+  x.w3 = *reinterpret_cast<const uint32_t*>(f + 12);
 #pragma unroll
-    for (int j = 16; j < kPrefixDw; j++) d[j] = 0;
-    const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
-    const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
-    const bool fast = !valid || (etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 && 14 + ip_len <= 64);
-    if (__all(fast)) {
-      process<true>(p, T, i, valid, L, d, pkt0, lane, lds_list[wave], lds_sum[wave]);
-    } else {
-      load_prefix<4, 6>(f, L, d);
-      process<false>(p, T, i, valid, L, d, pkt0, lane, lds_list[wave], lds_sum[wave]);
+  for (int k = 0; k < 3; k++) x.v[k] = *reinterpret_cast<const u32x4_a4*>(f + 16 + 16 * k);
+}
+
+DEV void fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, uint32_t L,
+                    const Prefix& x) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  uint32_t d[kPrefixDw];
+  d[0] = d[1] = d[2] = 0;  // MAC addresses: never read on this path
+  d[3] = x.w3 & ones((int)L - 12 < 0 ? 0 : (int)L - 12);
+#pragma unroll
+  for (int k = 1; k < 4; k++) {
+    const u32x4& v = x.v[k - 1];
+    d[4 * k + 0] = v.x & ones((int)L - (16 * k + 0) < 0 ? 0 : (int)L - (16 * k + 0));
+    d[4 * k + 1] = v.y & ones((int)L - (16 * k + 4) < 0 ? 0 : (int)L - (16 * k + 4));
+    d[4 * k + 2] = v.z & ones((int)L - (16 * k + 8) < 0 ? 0 : (int)L - (16 * k + 8));
+    d[4 * k + 3] = v.w & ones((int)L - (16 * k + 12) < 0 ? 0 : (int)L - (16 * k + 12));
+  }
+#pragma unroll
+  for (int j = 16; j < kPrefixDw; j++) d[j] = 0;
+  const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
+  const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
+  const bool fast = !valid || (L <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
+                               14 + ip_len <= 64);
+  const bool all_fast = __all(fast);
+  if (lane == 0) p.defer[chunk] = all_fast ? 0 : 1;
+  if (!all_fast) return;
+  process_fast(p, T, i, valid, L, d);
+}
+
+}  // namespace
+
+// AHEAD = how many chunks' prefixes a wave keeps in flight while it
+// computes one (register double/triple buffering); descriptors run one
+// stage further ahead because the prefix address depends on them.
+template <bool OFFS, int AHEAD>
+DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * kWaves;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  uint32_t Ld[AHEAD + 1];
+  uint64_t od[AHEAD + 1];
+  Prefix v[AHEAD];
+#pragma unroll
+  for (int a = 0; a <= AHEAD; a++) fetch_desc<OFFS>(p, c + a * nw, lane, Ld[a], od[a]);
+#pragma unroll
+  for (int a = 0; a < AHEAD; a++) fetch_prefix(p, c + a * nw, lane, Ld[a], od[a], v[a]);
+  for (;;) {
+    // chunks past the end read clamped descriptors and no frame bytes
+    uint32_t Ln;
+    uint64_t on;
+    fetch_desc<OFFS>(p, c + (AHEAD + 1) * nw, lane, Ln, on);
+    Prefix vn;
+    fetch_prefix(p, c + AHEAD * nw, lane, Ld[AHEAD], od[AHEAD], vn);
+    fast_chunk(p, T, c, lane, Ld[0], v[0]);
+    c += nw;
+    if (c >= nchunks) break;
+#pragma unroll
+    for (int a = 0; a < AHEAD; a++) {
+      Ld[a] = Ld[a + 1];
+      od[a] = od[a + 1];
+    }
+    Ld[AHEAD] = Ln;
+    od[AHEAD] = on;
+#pragma unroll
+    for (int a = 0; a + 1 < AHEAD; a++) v[a] = v[a + 1];
+    v[AHEAD - 1] = vn;
+  }
+}
+
+#define IXG_FAST_KERNEL(NAME, OFFS, AHEAD, WAVES)                                    \
+  extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
+  NAME(KParams p) {                                                                 \
+    __shared__ uint64_t T[12 * 256];                                                \
+    stage_tables(p, T);                                                             \
+    fast_loop<OFFS, AHEAD>(p, T);                                                   \
+  }
+
+// variants for A/B (IXGRX_FAST_VARIANT); index 0 is the default.
+// _s: fixed-stride layout, _o: u64 offsets
+IXG_FAST_KERNEL(ixg_rx_fast_s, false, 1, 5)
+IXG_FAST_KERNEL(ixg_rx_fast_o, true, 1, 5)
+IXG_FAST_KERNEL(ixg_rx_fast_a2w4_s, false, 2, 4)
+IXG_FAST_KERNEL(ixg_rx_fast_a2w4_o, true, 2, 4)
+IXG_FAST_KERNEL(ixg_rx_fast_a2w5_s, false, 2, 5)
+IXG_FAST_KERNEL(ixg_rx_fast_a2w5_o, true, 2, 5)
+IXG_FAST_KERNEL(ixg_rx_fast_a1w4_s, false, 1, 4)
+IXG_FAST_KERNEL(ixg_rx_fast_a1w4_o, true, 1, 4)
+
+// ---- general kernel --------------------------------------------------------
+// Every header shape the reference handles. Workgroup-lockstep over groups
+// of 256 chunks: the chunks the fixed-shape kernel flagged (p.defer[c] != 0,
+// or all when p.defer is null) are compacted into an LDS list, parsed four
+// at a time (one per wave, pass A), and the packets whose L4 segment runs
+// past the 96-byte prefix are streamed in pass B once 256 have accumulated.
+template <bool OFFS, int P>
+DEV void general_body(const KParams& p) {
+  __shared__ uint64_t T[12 * 256];
+  __shared__ uint32_t chunks[256];
+  __shared__ uint32_t n_chunks, n_long;
+  __shared__ uint32_t l_pkt[kLongCap], l_end[kLongCap], l_acc[kLongCap], l_ip[kLongCap];
+  __shared__ u32x4 l_ok[kLongCap], l_bad[kLongCap];
+  const LongList ll{LDS(lds_u32, &n_long), LDS(lds_u32, l_pkt), LDS(lds_u32, l_end), LDS(lds_u32, l_acc),
+                    LDS(lds_u32, l_ip), LDS(lds_u32x4, l_ok), LDS(lds_u32x4, l_bad)};
+  if (threadIdx.x == 0) n_long = 0;
+  stage_tables(p, T);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t ngroups = (nchunks + 255u) >> 8;
+  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    if (threadIdx.x == 0) n_chunks = 0;
+    __syncthreads();
+    const uint32_t ci = g * 256u + threadIdx.x;
+    const bool want = ci < nchunks && (p.defer == nullptr || p.defer[ci] != 0);
+    const uint64_t m = __ballot(want);
+    if (m) {
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(&n_chunks, (uint32_t)__popcll(m));
+      base = (uint32_t)__shfl((int)base, 0);
+      if (want) chunks[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+    }
+    __syncthreads();
+    const uint32_t nc = n_chunks;
+    for (uint32_t j = 0; j < nc; j += kWaves) {
+      if (j + wave < nc) pass_a_chunk<OFFS>(p, T, chunks[j + wave], lane, ll);
+      __syncthreads();
+      const uint32_t cnt = n_long;
+      if (cnt >= 256u || j + kWaves >= nc) {
+        if (cnt) pass_b<OFFS, P>(p, cnt, ll);
+        __syncthreads();
+        if (threadIdx.x == 0) n_long = 0;
+        __syncthreads();
+      }
     }
   }
 }
 
-extern "C" int ixgrx_launch(const void* params, uint32_t grid, void* stream) {
+#define IXG_GEN_KERNEL(NAME, OFFS, P) \
+  extern "C" __global__ void __launch_bounds__(kBlock) NAME(KParams p) { general_body<OFFS, P>(p); }
+IXG_GEN_KERNEL(ixg_rx_general_s, false, 8)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, 8)
+IXG_GEN_KERNEL(ixg_rx_general_p4_s, false, 4)
+IXG_GEN_KERNEL(ixg_rx_general_p4_o, true, 4)
+IXG_GEN_KERNEL(ixg_rx_general_p16_s, false, 16)
+IXG_GEN_KERNEL(ixg_rx_general_p16_o, true, 16)
+
+typedef void (*kern_fn)(KParams);
+// [variant][layout: 0 = stride, 1 = offsets]
+static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
+                                    {ixg_rx_fast_a2w4_s, ixg_rx_fast_a2w4_o},
+                                    {ixg_rx_fast_a2w5_s, ixg_rx_fast_a2w5_o},
+                                    {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}};
+static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
+                                   {ixg_rx_general_p4_s, ixg_rx_general_p4_o},
+                                   {ixg_rx_general_p16_s, ixg_rx_general_p16_o}};
+static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
+static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
+
+// variant = fast_variant | (general_variant << 8)
+extern "C" int ixgrx_launch(const void* params, int variant, uint32_t grid_fast, uint32_t grid_gen, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
-  hipLaunchKernelGGL(ixg_rx_kernel, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, p);
+  int fv = variant & 0xff, gv = (variant >> 8) & 0xff;
+  if (fv >= k_nfast) fv = 0;
+  if (gv >= k_ngen) gv = 0;
+  const int lay = p.off ? 1 : 0;
+  if (p.defer) hipLaunchKernelGGL(k_fast[fv][lay], dim3(grid_fast), dim3(kBlock), 0, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(k_gen[gv][lay], dim3(grid_gen), dim3(kBlock), 0, (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
 
 extern "C" uint32_t ixgrx_kparams_size(void) { return (uint32_t)sizeof(KParams); }
 
-extern "C" int ixgrx_blocks_per_cu(void) {
+extern "C" int ixgrx_blocks_per_cu(int which) {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ixg_rx_kernel, kBlock, 0) != hipSuccess || nb < 1)
-    nb = 1;
+  const int fv = which & 0xff;
+  hipError_t e = which >= 0 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_fast[fv < k_nfast ? fv : 0][0], kBlock, 0)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_gen[(-which - 1) < k_ngen ? (-which - 1) : 0][0], kBlock, 0);
+  if (e != hipSuccess || nb < 1) nb = 1;
   return nb;
 }
 extern "C" uint32_t ixgrx_block(void) { return (uint32_t)kBlock; }

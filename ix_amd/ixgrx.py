@@ -88,6 +88,15 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise RuntimeError(f"{path} missing: build it with __graft_entry__.build() "
                            "(make -C ix_amd/csrc)")
+    # PyTorch bundles its own libamdhip64.so.7. Loading torch first makes
+    # libixgrx's NEEDED entry resolve to that already-loaded runtime, so the
+    # process has ONE HIP runtime and torch's device pointers and streams
+    # are valid for the kernels. (The reverse order leaves torch unable to
+    # initialise.) Pure C consumers simply use /opt/rocm's runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     lib.ixg_rx_init.argtypes = [ctypes.POINTER(RxCfg), i32, ctypes.POINTER(vp)]

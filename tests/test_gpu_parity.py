@@ -34,14 +34,24 @@ def _diff(got, exp, what):
                           f"gpu {g[bad[0]].tolist()} vs exp {exp[bad[0]].tolist()}"
 
 
-@pytest.fixture(scope="module")
-def engines():
+@pytest.fixture(scope="module", params=["auto", "general"])
+def engines(request):
+    """Engines on the default path (fixed-shape kernel + general kernel for
+    flagged chunks) and with IXGRX_FORCE_GENERAL=1 (general kernel only)."""
     cache = {}
 
     def get(key=KEY, nb=128, dev=0, flags=0):
         k = (bytes(key), nb, dev, flags)
         if k not in cache:
-            cache[k] = ixgrx.RxEngine(ixgrx.Config(bytes(key), nb, dev, flags))
+            old = os.environ.get("IXGRX_FORCE_GENERAL")
+            os.environ["IXGRX_FORCE_GENERAL"] = "1" if request.param == "general" else "0"
+            try:
+                cache[k] = ixgrx.RxEngine(ixgrx.Config(bytes(key), nb, dev, flags))
+            finally:
+                if old is None:
+                    del os.environ["IXGRX_FORCE_GENERAL"]
+                else:
+                    os.environ["IXGRX_FORCE_GENERAL"] = old
         return cache[k]
     yield get
     for e in cache.values():
