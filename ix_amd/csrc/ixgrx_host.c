@@ -24,6 +24,7 @@ struct ixg_ctx {
 	int force_general;   /* IXGRX_FORCE_GENERAL=1: skip the fixed-shape kernel (tests/A-B) */
 	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
 	uint8_t *d_defer;    /* one flag per 64-packet chunk */
+	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
 	size_t defer_cap;
 	uint64_t *d_tab;
 	uint32_t *d_tab6;
@@ -142,6 +143,7 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_tab);
 	hipFree(c->d_tab6);
 	hipFree(c->d_defer);
+	hipFree(c->d_zero);
 	hipFree(c->d_frames);
 	hipFree(c->d_off);
 	hipFree(c->d_len);
@@ -217,6 +219,9 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		}
 		free(t6);
 	}
+	if (hipMalloc((void **)&c->d_zero, IXG_ZERO_PAGE) != hipSuccess ||
+	    hipMemset(c->d_zero, 0, IXG_ZERO_PAGE) != hipSuccess)
+		goto fail;
 	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
 	*out = c;
@@ -246,6 +251,7 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 	p.flags = c->cfg.flags;
 	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
 	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
+	p.zero = c->d_zero;
 	size_t nchunks = ((size_t)n + 63) / 64;
 	if (!c->force_general) {
 		if (nchunks > c->defer_cap) {
@@ -261,7 +267,7 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 	}
 	uint32_t blk = ixgrx_block();
 	uint64_t want_f = (nchunks + blk / 64 - 1) / (blk / 64);     /* one wave per chunk */
-	uint64_t want_g = (nchunks + 255) / 256;                          /* one workgroup per 256 chunks */
+	uint64_t want_g = (((nchunks + 63) / 64) + blk / 64 - 1) / (blk / 64); /* one wave per 64 chunks */
 	uint32_t gf = want_f < c->grid_fast ? (uint32_t)want_f : c->grid_fast;
 	uint32_t gg = want_g < c->grid_gen ? (uint32_t)want_g : c->grid_gen;
 	if (gf == 0)

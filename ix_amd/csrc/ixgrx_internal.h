@@ -28,8 +28,12 @@ struct ixg_kparams {
 	uint32_t fg_mask;      /* nb_rx_fgs - 1 */
 	uint8_t *defer;        /* per 64-packet chunk: 1 = left for the general
 	                          kernel; NULL = general kernel does everything */
+	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
+	                          loads that must read nothing */
 };
 typedef struct ixg_kparams ixg_kparams;
+
+#define IXG_ZERO_PAGE 4096u
 
 /* implemented in ixgrx_kernels.hip */
 int ixgrx_launch(const void *params, int fast_variant, uint32_t grid_fast, uint32_t grid_gen, void *stream);

@@ -129,13 +129,16 @@ struct LaneState {
   bool v6;
 };
 
-template <bool FAST>
+// FIXED: every lane is IPv4 with ihl 5 (wave-uniform), so the header
+// geometry is constant-folded. NDW: prefix dwords available; a segment
+// ending past 4*NDW bytes is left to the streaming rounds.
+template <bool FIXED, int NDW>
 DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint32_t (&d)[kPrefixDw],
                     uint32_t L, LaneState& s) {
   const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);       // ip.c:132
   const uint32_t vh = byte_at(d, 14);
   const uint32_t ver = vh >> 4;
-  const int ihl = FAST ? 5 : (int)(vh & 15u);                             // ip.h:84-90
+  const int ihl = FIXED ? 5 : (int)(vh & 15u);                             // ip.h:84-90
   const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
   const uint32_t ip_off = (byte_at(d, 20) << 8) | byte_at(d, 21);
   const uint32_t proto = byte_at(d, 23);
@@ -144,12 +147,12 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   const uint32_t dst = (d[7] >> 16) | (d[8] << 16);                       // bytes 30..33 raw
   const int l4 = 14 + 4 * ihl;
   const bool ip4 = etype == 0x0800u;
-  const bool v6 = !FAST && etype == 0x86DDu && (p.flags & IXG_F_IPV6);
+  const bool v6 = !FIXED && etype == 0x86DDu && (p.flags & IXG_F_IPV6);
 
   // L4 header dwords: frame byte l4+b sits in dword q + (2+b)/4
   const int q = 3 + (ihl < 5 ? 5 : ihl);
   uint32_t h0, h1, h3;
-  if (FAST) {
+  if (FIXED) {
     h0 = d[8]; h1 = d[9]; h3 = d[11];
   } else {
     h0 = pick<kPrefixDw, 8, 18>(d, q);
@@ -175,7 +178,7 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   s.ip_res = 0xffffu;
   if (hdr_ok) {
     uint64_t hs;
-    if (FAST) {
+    if (FIXED) {
       hs = (uint64_t)(d[3] >> 16) + d[4] + d[5] + d[6] + d[7] + (d[8] & 0xffffu);
     } else {
       hs = region_sum(d, 3, l4);
@@ -237,23 +240,18 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
 
   const uint32_t sp = s.proto;
   // UDP checksum field: L4 bytes 6,7 = low half of dword q+2
-  const uint32_t ucs = v6 ? 1u : (pick<kPrefixDw, 10, 20>(d, q + 2) & 0xffffu);
+  const uint32_t ucs = v6 ? 1u : ((FIXED ? d[10] : pick<kPrefixDw, 10, 20>(d, q + 2)) & 0xffffu);
   int kind = 0;
   if (seg_ok && ((sp == 6 && l4len >= 20) || (sp == 17 && l4len >= 8 && ucs != 0))) kind = 1;
   if (!v6 && seg_ok && sp == 1 && l4len >= 8) kind = 2;
   s.l4_kind = kind;
   uint64_t acc = 0;
   if (kind) {
-    const int e = (int)(seg_end < (uint32_t)(FAST ? 4 * kFastDw : kStreamBase) ? seg_end
-                                                                             : (FAST ? 4 * kFastDw : kStreamBase));
-    if (FAST) {
-      uint32_t dd[kFastDw];
+    const int e = (int)(seg_end < (uint32_t)(4 * NDW) ? seg_end : (uint32_t)(4 * NDW));
+    uint32_t dd[NDW];
 #pragma unroll
-      for (int j = 0; j < kFastDw; j++) dd[j] = d[j];
-      acc = region_sum(dd, 8, e);
-    } else {
-      acc = region_sum(d, qa, e);
-    }
+    for (int j = 0; j < NDW; j++) dd[j] = d[j];
+    acc = region_sum(dd, FIXED ? 8 : qa, e);
     if (kind == 1) {
       uint64_t ps;
       if (v6) {
@@ -265,8 +263,7 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
     }
   }
   s.l4_acc = acc;
-  s.stream = kind != 0 && seg_end > (uint32_t)kStreamBase;
-  if (FAST) s.stream = false;
+  s.stream = kind != 0 && seg_end > (uint32_t)(4 * NDW);
 }
 
 // The record for a lane given its L4 residual: the residual computed, or a
@@ -392,76 +389,18 @@ DEV void load_prefix(const uint8_t* f, uint32_t L, const uint8_t* dummy, uint32_
 DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, bool valid, uint32_t L,
                       const uint32_t (&d)[kPrefixDw]) {
   LaneState s;
-  lane_parse<true>(p, T, d, L, s);
+  lane_parse<true, kFastDw>(p, T, d, L, s);
   if (valid) {
     const uint32_t r4 = l4_residual(s);
     store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
   }
 }
 
-// ---- general path: pass A (lane per packet, 96-byte prefix) + pass B
-// (segments past the prefix, compacted into a per-workgroup LDS list and
-// streamed lane-per-packet with U 16-byte loads in flight per lane).
-constexpr int kLongCap = 512;  // list capacity; flushed at >= 256 entries
-
 // LDS (address space 3) pointers: through generic pointers these would be
 // flat_* accesses, which count on vmcnt as well and force vmcnt(0) waits
 // that serialise the streaming loads.
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 #define LDS(T, x) ((T*)(x))
-
-struct LongList {
-  lds_u32* cnt;
-  lds_u32* pkt;     // packet index
-  lds_u32* end;     // segment end (frame offset)
-  lds_u32* acc;     // folded sum of the in-prefix part + pseudo header
-  lds_u32* ipres;   // IP header residual (csum output)
-  lds_u32x4* rec_ok;   // record if the L4 residual is 0
-  lds_u32x4* rec_bad;  // record if it is not
-};
-
-template <bool OFFS>
-DEV void pass_a_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
-                      const LongList& ll) {
-  const uint32_t i = chunk * 64u + (uint32_t)lane;
-  const bool valid = i < p.n;
-  const uint32_t ic = valid ? i : p.n - 1;  // clamped: descriptor loads without a branch
-  const uint32_t L = valid ? (uint32_t)p.len[ic] : 0u;
-  const uint8_t* f = p.base + frame_off<OFFS>(p, ic);
-  uint32_t d[kPrefixDw];
-  load_prefix<0, 6>(f, L, reinterpret_cast<const uint8_t*>(p.tab), d);
-  LaneState s;
-  lane_parse<false>(p, T, d, L, s);
-  const bool lng = valid && s.stream;
-  const uint64_t m = __ballot(lng);
-  if (m) {
-    uint32_t base = 0;
-    if (lane == 0) base = __hip_atomic_fetch_add(ll.cnt, (uint32_t)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    base = (uint32_t)__shfl((int)base, 0);
-    if (lng) {
-      const uint32_t e = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      ll.pkt[e] = i;
-      ll.end[e] = s.seg_end;
-      ll.acc[e] = fold32(s.l4_acc);
-      ll.ipres[e] = s.ip_res;
-      const Rec ok = make_record(p, d, L, s, 0u), bad = make_record(p, d, L, s, 1u);
-      ll.rec_ok[e] = u32x4{ok.w0, ok.w1, ok.w2, ok.w3};
-      ll.rec_bad[e] = u32x4{bad.w0, bad.w1, bad.w2, bad.w3};
-    }
-  }
-  if (valid && !lng) {
-    const uint32_t r4 = l4_residual(s);
-    store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
-  }
-}
-
-// end-around sum over the whole wave (every lane gets the total)
-DEV uint32_t wave_sum1c(uint32_t a) {
-#pragma unroll
-  for (int m = 1; m < 64; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, 64));
-  return a;
-}
 
 // masked sum of a 16-byte piece whose first byte is `rem` bytes before the
 // segment end (rem <= 0: nothing of it is inside)
@@ -470,69 +409,153 @@ DEV uint64_t piece_sum(const u32x4& v, int rem) {
          (v.z & ones(rem - 8 < 0 ? 0 : rem - 8)) + (v.w & ones(rem - 12 < 0 ? 0 : rem - 12));
 }
 
-// Pass B: one wave per packet, its segment tail [96, end) read as fully
-// coalesced 1 KiB wave-instructions; the loads of P packets are issued
-// before the first reduction. Entries are dealt to waves round-robin.
-template <bool OFFS, int P>
-DEV void pass_b(const KParams& p, uint32_t cnt, const LongList& ll) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int kPiece = 2;  // 2 KiB per packet per pass: frames up to 2144 B in one pass
-  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(p.tab) + 16 * lane;
-  for (uint32_t k0 = (uint32_t)wave; k0 < cnt; k0 += kWaves * P) {
-    uint32_t ends[P];
-    uint64_t offs[P];
+// ---- general path -------------------------------------------------------
+// Pass A: lane per packet, 96-byte prefix, full parse. Lanes whose L4
+// segment runs past the prefix ("long") are compacted per wave (ballot +
+// mbcnt) into an LDS list and their tails [96, end) are streamed by groups
+// of kG lanes, kRoundPk packets per round, kT 16-byte loads per lane per
+// round (2 KiB per packet). Rounds use two register buffers A/B whose loads
+// are always issued (dummy when a group has no packet), so hipcc's vmcnt
+// waits for one buffer never cover the other.
+constexpr int kG = 16;
+constexpr int kRoundPk = 64 / kG;
+constexpr int kT = 8;
+
+struct WaveLds {  // per-wave scratch, LDS address space
+  lds_u32* list;  // compacted long lanes
+  lds_u32* end;   // per lane: segment end
+  lds_u32* offlo; // per lane: frame offset (low/high words)
+  lds_u32* offhi;
+  lds_u32* sum;   // per lane: streamed tail sum
+};
+
+struct Round {
+  u32x4 v[kT];
+  uint32_t end;   // owner's segment end (0: this group has no packet)
+  uint32_t owner;
+};
+
+DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, uint32_t nlong, int lane, Round& b) {
+  const int g = lane / kG, gl = lane % kG;
+  const uint32_t k = r * kRoundPk + (uint32_t)g;
+  const bool act = k < nlong;
+  const uint32_t owner = w.list[act ? k : 0u];
+  b.owner = owner;
+  b.end = act ? w.end[owner] : 0u;
+  const uint64_t off = ((uint64_t)w.offhi[owner] << 32) | w.offlo[owner];
+  const uint8_t* f = p.base + off;
+  // pieces at or past the segment end read the zero page: they add nothing
+  const uint8_t* zero = p.zero + 16 * lane;
 #pragma unroll
-    for (int j = 0; j < P; j++) {  // addresses first (uniform: LDS broadcast + scalar loads)
-      const uint32_t e = k0 + (uint32_t)(kWaves * j);
-      const uint32_t ec = e < cnt ? e : 0u;
-      ends[j] = e < cnt ? ll.end[ec] : 0u;
-      const uint32_t pk = __builtin_amdgcn_readfirstlane(ll.pkt[ec]);
-      offs[j] = frame_off<OFFS>(p, pk);
+  for (int t = 0; t < kT; t++) {
+    const uint32_t pos = kStreamBase + 16u * gl + 16u * kG * t;
+    b.v[t] = load16(pos < b.end, f + pos, zero);
+  }
+}
+
+// b.v[t] for a per-lane t in [0, kT): binary mux on the bits of t (a ?:
+// chain indexed by t would be turned back into a scratch-memory access)
+DEV u32x4 pick_piece(const u32x4 (&v)[kT], uint32_t t) {
+  static_assert(kT == 8, "3-level mux");
+  const bool b0 = t & 1u, b1 = t & 2u, b2 = t & 4u;
+  const u32x4 a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
+  const u32x4 c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
+  return b2 ? c1 : c0;
+}
+
+DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round& b) {
+  const int gl = lane % kG;
+  // every piece is either inside the segment or zero: plain 32-bit word sum
+  uint64_t acc = 0;
+#pragma unroll
+  for (int t = 0; t < kT; t++) acc += (uint64_t)b.v[t].x + b.v[t].y + b.v[t].z + b.v[t].w;
+  // except the one piece that straddles the end: take back its bytes >= end
+  const int rem0 = (int)b.end - (int)(kStreamBase + 16u * gl);
+  const uint32_t r = (uint32_t)rem0 & 255u, tb = (uint32_t)rem0 >> 8;
+  if (rem0 > 0 && r != 0u && r < 16u && tb < (uint32_t)kT) {
+    const u32x4 vb = pick_piece(b.v, tb);
+    const int ri = (int)r;
+    acc -= (uint64_t)(vb.x & ~ones(ri)) + (vb.y & ~ones(ri - 4 < 0 ? 0 : ri - 4)) +
+           (vb.z & ~ones(ri - 8 < 0 ? 0 : ri - 8)) + (vb.w & ~ones(ri - 12 < 0 ? 0 : ri - 12));
+  }
+  uint32_t a = fold32(acc);
+  // frames longer than 96 + 2 KiB (not IX mbufs): the rest, synchronously
+  const uint32_t more = kStreamBase + 16u * kG * kT;
+  if (__any(b.end > more)) {
+    const uint64_t off = ((uint64_t)w.offhi[b.owner] << 32) | w.offlo[b.owner];
+    const uint8_t* zero = p.zero + 16 * lane;
+    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 16u * kG) {
+      const uint32_t pos = pos0 + 16u * gl;
+      const u32x4 v = load16(pos < b.end, p.base + off + pos, zero);
+      a = add1c(a, fold32(piece_sum(v, (int)b.end - (int)pos)));
     }
-    u32x4 v[P][kPiece];
+  }
 #pragma unroll
-    for (int j = 0; j < P; j++) {  // then every packet's loads, back to back
-#pragma unroll
-      for (int t = 0; t < kPiece; t++) {
-        const uint32_t pos = kStreamBase + 16u * lane + 1024u * t;
-        v[j][t] = load16(pos < ends[j], p.base + offs[j] + pos, dummy);
-      }
+  for (int m = 1; m < kG; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, kG));
+  if (gl == 0 && b.end != 0u) w.sum[b.owner] = a;
+}
+
+template <bool OFFS>
+DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
+                       const WaveLds& w) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t ic = valid ? i : p.n - 1;  // clamped: descriptor loads without a branch
+  const uint32_t L = valid ? (uint32_t)p.len[ic] : 0u;
+  const uint64_t off = frame_off<OFFS>(p, ic);
+  uint32_t d[kPrefixDw];
+  load_prefix<0, 6>(p.base + off, L, reinterpret_cast<const uint8_t*>(p.tab), d);
+  LaneState s;
+  const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
+  if (__all(fixed))
+    lane_parse<true, kPrefixDw>(p, T, d, L, s);
+  else
+    lane_parse<false, kPrefixDw>(p, T, d, L, s);
+  const bool lng = valid && s.stream;
+  const uint64_t m = __ballot(lng);
+  if (!m) {  // no long segment in this chunk (wave-uniform)
+    if (valid) {
+      const uint32_t r4 = l4_residual(s);
+      store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
     }
-    uint32_t part[P];
-#pragma unroll
-    for (int j = 0; j < P; j++) {
-      uint64_t acc = 0;
-#pragma unroll
-      for (int t = 0; t < kPiece; t++)
-        acc += piece_sum(v[j][t], (int)ends[j] - (int)(kStreamBase + 16u * lane + 1024u * t));
-      part[j] = fold32(acc);
-    }
-    // frames longer than 96 + 2 KiB (not IX mbufs, whose data is <= 2048 B):
-    // the rest, one KiB at a time, after the batch so the common path keeps
-    // all P packets' loads in flight together
-    uint32_t emax = 0;
-#pragma unroll
-    for (int j = 0; j < P; j++) emax = ends[j] > emax ? ends[j] : emax;
-    if (emax > kStreamBase + 1024u * kPiece) {
-#pragma unroll
-      for (int j = 0; j < P; j++) {
-        for (uint32_t pos0 = kStreamBase + 1024u * kPiece; pos0 < ends[j]; pos0 += 1024u) {
-          const uint32_t pos = pos0 + 16u * lane;
-          const u32x4 w = load16(pos < ends[j], p.base + offs[j] + pos, dummy);
-          part[j] = add1c(part[j], fold32(piece_sum(w, (int)ends[j] - (int)pos)));
-        }
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < P; j++) {
-      const uint32_t e = k0 + (uint32_t)(kWaves * j);
-      const uint32_t tot = wave_sum1c(part[j]);
-      if (lane == 0 && e < cnt) {
-        const uint32_t res = (~fold16(add1c(ll.acc[e], tot))) & 0xffffu;
-        const uint32_t i = ll.pkt[e];
-        *reinterpret_cast<u32x4*>(p.out + i) = res == 0 ? ll.rec_ok[e] : ll.rec_bad[e];
-        if (p.csum) p.csum[i] = ll.ipres[e] | (res << 16);
-      }
+    return;
+  }
+  // records for both outcomes of the pending L4 check; then only these
+  // few registers stay live across the streaming rounds
+  const uint32_t r4 = lng ? 0u : l4_residual(s);
+  Rec rok = make_record(p, d, L, s, r4);
+  Rec rbad = make_record(p, d, L, s, 1u);
+  uint32_t acc32 = fold32(s.l4_acc), ip_res = s.ip_res;
+  // materialise these now, so the parse state (d[], s) is dead during the
+  // streaming rounds instead of being kept live for sunk computations
+  asm volatile("" : "+v"(rok.w0), "+v"(rok.w1), "+v"(rok.w2), "+v"(rok.w3));
+  asm volatile("" : "+v"(rbad.w0), "+v"(rbad.w1), "+v"(rbad.w2), "+v"(rbad.w3));
+  asm volatile("" : "+v"(acc32), "+v"(ip_res));
+  if (lng) {
+    w.list[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)lane;
+    w.end[lane] = s.seg_end;
+    w.offlo[lane] = (uint32_t)off;
+    w.offhi[lane] = (uint32_t)(off >> 32);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t nlong = (uint32_t)__popcll(m);
+  const uint32_t R = (nlong + kRoundPk - 1) / kRoundPk;
+  Round A, B;
+  round_issue(p, w, 0, nlong, lane, A);
+#pragma clang loop unroll(disable)
+  for (uint32_t r = 0; r < R; r += 2) {
+    round_issue(p, w, r + 1, nlong, lane, B);
+    round_finish(p, w, lane, A);
+    round_issue(p, w, r + 2, nlong, lane, A);
+    round_finish(p, w, lane, B);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (valid) {
+    if (lng) {
+      const uint32_t res = (~fold16(add1c(acc32, w.sum[lane]))) & 0xffffu;
+      store_record(p, i, res == 0 ? rok : rbad, ip_res, res);
+    } else {
+      store_record(p, i, rok, ip_res, r4);
     }
   }
 }
@@ -575,7 +598,8 @@ DEV void fetch_prefix(const KParams& p, uint32_t chunk, int lane, uint32_t L, ui
   const uint32_t i = chunk * 64u + (uint32_t)lane;
   // only frames that can be fast are worth loading; the bytes may run past
   // L into the next frame or the tail pad (include/ixgrx.h IXG_TAIL_PAD)
-  const bool ok = i < p.n && L <= 64u;
+  // decided per wave: a chunk with any longer frame is deferred anyway
+  const bool ok = i < p.n && __all(L <= 64u || i >= p.n);
   const uint8_t* f = ok ? p.base + o : reinterpret_cast<const uint8_t*>(p.tab);
   x.w3 = *reinterpret_cast<const uint32_t*>(f + 12);
 #pragma unroll
@@ -671,61 +695,37 @@ IXG_FAST_KERNEL(ixg_rx_fast_a1w4_s, false, 1, 4)
 IXG_FAST_KERNEL(ixg_rx_fast_a1w4_o, true, 1, 4)
 
 // ---- general kernel --------------------------------------------------------
-// Every header shape the reference handles. Workgroup-lockstep over groups
-// of 256 chunks: the chunks the fixed-shape kernel flagged (p.defer[c] != 0,
-// or all when p.defer is null) are compacted into an LDS list, parsed four
-// at a time (one per wave, pass A), and the packets whose L4 segment runs
-// past the 96-byte prefix are streamed in pass B once 256 have accumulated.
-template <bool OFFS, int P>
+// Every header shape the reference handles. Waves scan the defer flags 64
+// chunks at a time and process the flagged chunks (all chunks when
+// p.defer is null) one at a time.
+template <bool OFFS>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
-  __shared__ uint32_t chunks[256];
-  __shared__ uint32_t n_chunks, n_long;
-  __shared__ uint32_t l_pkt[kLongCap], l_end[kLongCap], l_acc[kLongCap], l_ip[kLongCap];
-  __shared__ u32x4 l_ok[kLongCap], l_bad[kLongCap];
-  const LongList ll{LDS(lds_u32, &n_long), LDS(lds_u32, l_pkt), LDS(lds_u32, l_end), LDS(lds_u32, l_acc),
-                    LDS(lds_u32, l_ip), LDS(lds_u32x4, l_ok), LDS(lds_u32x4, l_bad)};
-  if (threadIdx.x == 0) n_long = 0;
+  __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
+      sh_sum[kWaves][64];
   stage_tables(p, T);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
+                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave])};
+  const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t ngroups = (nchunks + 255u) >> 8;
-  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    if (threadIdx.x == 0) n_chunks = 0;
-    __syncthreads();
-    const uint32_t ci = g * 256u + threadIdx.x;
+  const uint32_t ngroups = (nchunks + 63u) >> 6;
+  for (uint32_t g = blockIdx.x * kWaves + wave; g < ngroups; g += nw) {
+    const uint32_t ci = g * 64u + (uint32_t)lane;
     const bool want = ci < nchunks && (p.defer == nullptr || p.defer[ci] != 0);
-    const uint64_t m = __ballot(want);
-    if (m) {
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(&n_chunks, (uint32_t)__popcll(m));
-      base = (uint32_t)__shfl((int)base, 0);
-      if (want) chunks[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
-    }
-    __syncthreads();
-    const uint32_t nc = n_chunks;
-    for (uint32_t j = 0; j < nc; j += kWaves) {
-      if (j + wave < nc) pass_a_chunk<OFFS>(p, T, chunks[j + wave], lane, ll);
-      __syncthreads();
-      const uint32_t cnt = n_long;
-      if (cnt >= 256u || j + kWaves >= nc) {
-        if (cnt) pass_b<OFFS, P>(p, cnt, ll);
-        __syncthreads();
-        if (threadIdx.x == 0) n_long = 0;
-        __syncthreads();
-      }
+    uint64_t m = __ballot(want);
+    while (m) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      general_chunk<OFFS>(p, T, g * 64u + b, lane, w);
     }
   }
 }
 
-#define IXG_GEN_KERNEL(NAME, OFFS, P) \
-  extern "C" __global__ void __launch_bounds__(kBlock) NAME(KParams p) { general_body<OFFS, P>(p); }
-IXG_GEN_KERNEL(ixg_rx_general_s, false, 8)
-IXG_GEN_KERNEL(ixg_rx_general_o, true, 8)
-IXG_GEN_KERNEL(ixg_rx_general_p4_s, false, 4)
-IXG_GEN_KERNEL(ixg_rx_general_p4_o, true, 4)
-IXG_GEN_KERNEL(ixg_rx_general_p16_s, false, 16)
-IXG_GEN_KERNEL(ixg_rx_general_p16_o, true, 16)
+#define IXG_GEN_KERNEL(NAME, OFFS) \
+  extern "C" __global__ void __launch_bounds__(kBlock) NAME(KParams p) { general_body<OFFS>(p); }
+IXG_GEN_KERNEL(ixg_rx_general_s, false)
+IXG_GEN_KERNEL(ixg_rx_general_o, true)
 
 typedef void (*kern_fn)(KParams);
 // [variant][layout: 0 = stride, 1 = offsets]
@@ -733,9 +733,7 @@ static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
                                     {ixg_rx_fast_a2w4_s, ixg_rx_fast_a2w4_o},
                                     {ixg_rx_fast_a2w5_s, ixg_rx_fast_a2w5_o},
                                     {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}};
-static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
-                                   {ixg_rx_general_p4_s, ixg_rx_general_p4_o},
-                                   {ixg_rx_general_p16_s, ixg_rx_general_p16_o}};
+static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o}};
 static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
 static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
 
