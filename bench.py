@@ -28,6 +28,11 @@ sys.path.insert(0, ROOT)
 METRIC = "Mpkt/s + GB/s device-resident RX parse+cksum+flow-hash, 64B & 1500B frames"
 PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
+# one ixg_rx_batch_dev launch = the fixed-shape kernel + the general kernel
+# (which, when no chunk was deferred, only scans the per-chunk flags); the
+# HIP events bracket both on the launch stream
+KERNELS = {False: "ixg_rx_fast_s + ixg_rx_general_s", True: "ixg_rx_fast_o + ixg_rx_general_o"}
+
 WORKLOADS = {
     # name: (trace kind, frames per GPU, distinct frames in the pool, description)
     "c2": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2: 16M x 64B Eth/IPv4/TCP frames (L=60, stride 60), 1 GPU"),
@@ -131,18 +136,60 @@ def time_steps(wl, eng, steps, warmup, dist, world):
     return el, float(np.mean(kern)), float(np.min(kern))
 
 
-def cpu_baseline(tr, flags, key, seconds: float, threads: int):
-    """The oracle (C restatement, table-driven hashes) on host cores over a
-    bounded sample of the same workload (its pool of distinct frames)."""
+def mbuf_arena(tr, n: int):
+    """The first n frames of `tr` laid out as IX mbufs (2112-B elements, len
+    @0, data @+64; inc/ix/mbuf.h:73-90). Returns (arena, pointers)."""
+    S = 2112
+    arena = np.zeros(n * S + 64, dtype=np.uint8)
+    base = (-arena.ctypes.data) % 64
+    rows = arena[base:base + n * S].reshape(n, S)
+    offs = tr.offsets()[:n].astype(np.int64)
+    lens = tr.len[:n].astype(np.int64)
+    rows[:, :8] = lens.astype("<u8").view(np.uint8).reshape(n, 8)
+    for L in np.unique(lens):
+        idx = np.nonzero(lens == L)[0]
+        src = offs[idx, None] + np.arange(L, dtype=np.int64)[None, :]
+        rows[idx, 64:64 + L] = tr.blob[src]
+    ptrs = arena.ctypes.data + base + np.arange(n, dtype=np.uint64) * S
+    return arena, ptrs
+
+
+def cpu_rate(ptrs, flags, key, seconds, threads, hash_mode, work):
     from oracle import oracle
     done, t0 = 0, time.perf_counter()
     while True:
-        oracle.rx_trace(tr, key, flags=flags, threads=threads, hash_mode=oracle.HASH_TABLE)
-        done += tr.n
+        oracle.rx_mbufs(key, 128, 0, flags, ptrs, threads=threads, hash_mode=hash_mode, work=work)
+        done += len(ptrs)
         el = time.perf_counter() - t0
         if el >= seconds:
-            break
-    return done / el / 1e6, done, el
+            return done / el / 1e6, done, el
+
+
+def cpu_baseline(tr, flags, key, seconds: float, threads: int, name: str):
+    """The oracle (C restatement) on host cores over a bounded sample of the
+    workload: its distinct frames (up to 2^20) in IX mbufs, repeated for
+    `seconds`. `value` = full software work (parse + IP/L4 checksums +
+    Toeplitz + tcp_to_idx, table-driven hashes) on `threads` threads; the
+    1-core modes of BASELINE.md's CPU plan and the reference's own code
+    (oracle/_ref, 1 core) are reported beside it."""
+    from oracle import oracle
+    n = min(tr.n, 1 << 20)
+    arena, ptrs = mbuf_arena(tr, n)
+    v, done, secs = cpu_rate(ptrs, flags, key, seconds, threads, oracle.HASH_TABLE, oracle.WORK_FULL)
+    side = max(1.0, seconds / 6)
+    one = {}
+    for label, hm, wk in (("full_table", oracle.HASH_TABLE, oracle.WORK_FULL),
+                          ("full_bitserial", oracle.HASH_BITSERIAL, oracle.WORK_FULL),
+                          ("ix_equivalent", oracle.HASH_TABLE, oracle.WORK_IX)):
+        one[label] = round(cpu_rate(ptrs[:1 << 16], flags, key, side, 1, hm, wk)[0], 2)
+    del arena
+    ref, rdesc = oracle.ref_time(tr, key, side, flags=flags)
+    return {"value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/ixgrx_oracle.c full software (table-driven Toeplitz/CRC) over {n} {name} frames "
+                      f"in 2112-B IX mbufs, {done} frames in {secs:.1f}s on {threads} threads",
+            "modes_1core_mpps": one,
+            "reference_1core_mpps": None if ref is None else round(ref / 1e6, 2),
+            "reference_sample": rdesc}
 
 
 def copy_inclusive(wl, eng, key, reps=3):
@@ -246,7 +293,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": PEAK_HBM_GBPS, "unit": "GB/s",
                      "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
                      "alg_bytes_per_pkt": round(wl.bytes_per_pkt, 2), "kernel_ms_avg": round(kavg * 1e3, 4),
-                     "kernel_ms_min": round(kmin * 1e3, 4), "kernel": "ixg_rx_kernel",
+                     "kernel_ms_min": round(kmin * 1e3, 4),
+                     "kernel": KERNELS[wl.off is not None],
                      "traffic_source": tsrc},
         "parity": "ok" if ok else "MISMATCH",
     }
@@ -273,12 +321,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = min(16, os.cpu_count() or 1)
         pname, ptr, pflags = primary
-        v, done, secs = cpu_baseline(ptr, pflags, key, args.cpu_seconds, threads)
-        v1, done1, secs1 = cpu_baseline(ptr, pflags, key, max(2.0, args.cpu_seconds / 4), 1)
-        res["cpu_baseline"] = {"value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
-                               "sample": f"oracle/ixgrx_oracle.c (table-driven hashes) over {done} frames "
-                                         f"of the {pname} pool in {secs:.1f}s",
-                               "value_1core": round(v1, 2)}
+        res["cpu_baseline"] = cpu_baseline(ptr, pflags, key, args.cpu_seconds, threads, pname)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -1,22 +1,27 @@
 // ixgrx_kernels.hip - MI355X (gfx950) RX parse + checksum + flow-hash kernels.
 //
-// One wavefront lane per packet. Each lane loads the first 96 bytes of its
-// frame as 16-byte vector loads (header prefix; the IPv4 header with options
-// and every L4 header field the path reads sit inside it), parses
-// Ethernet/IPv4/TCP/UDP/ICMP exactly as dp/net/ip.c + dp/lwip do, sums the
-// IP header and the in-prefix part of the L4 segment as 32-bit one's
-// complement words, and looks the 12 tuple bytes up in a per-workgroup LDS
-// copy of the combined Toeplitz/CRC-32C byte tables (both hashes are
-// GF(2)-affine in the tuple, DESIGN.md "hash tables"). Segments that extend
-// past the prefix (IMIX, 1500 B frames) are compacted per wave with
-// ballot/mbcnt into an LDS list and summed cooperatively: 16 lanes (one DPP
-// row) per packet, 256 contiguous bytes per wave-instruction per packet,
-// up to 8 loads in flight per lane, then a row reduction.
+// Two kernels per batch, both one wavefront lane per packet:
 //
-// A wave whose 64 packets are all plain IPv4 (ihl 5, segment ending inside
-// the first 64 bytes: the 64 B TCP config) takes an instantiation where the
-// header geometry is constant-folded. Both instantiations produce identical
-// records (same code, template on a constant).
+// ixg_rx_fast_{s,o}: the fixed-shape kernel. A persistent grid-stride loop
+// over 64-packet chunks, software-pipelined: descriptors two chunks ahead,
+// the 52 header bytes a 64 B frame needs (12..63) one chunk ahead. A chunk
+// whose 64 frames are all plain IPv4 ihl 5 with the segment inside 64
+// bytes (the 64 B TCP config) is parsed with the header geometry
+// constant-folded; any other chunk is flagged in the per-chunk defer array.
+//
+// ixg_rx_general_{s,o}: every header shape the reference handles, for the
+// flagged chunks (or all chunks when the fixed-shape kernel is skipped).
+// Pass A: each lane loads its 96-byte prefix, parses Ethernet/IPv4 (with
+// options)/TCP/UDP/ICMP (and the IPv6 extension) as dp/net/ip.c + dp/lwip
+// do, and sums the IP header and the in-prefix part of the L4 segment as
+// 32-bit one's complement words. Segments running past the prefix are
+// compacted per wave (ballot + mbcnt) into an LDS list; their tails are
+// summed by 16-lane groups, 4 packets per round, 8 x 16 B loads per lane
+// per round, two rounds in flight, then a 16-lane shuffle reduction.
+//
+// Both kernels look the 12 tuple bytes up in a per-workgroup LDS copy of
+// the combined Toeplitz/CRC-32C byte tables (both hashes are GF(2)-affine
+// in the tuple, DESIGN.md "hash tables").
 //
 // No MFMA: this is integer byte work bound by HBM bandwidth.
 #include <hip/hip_runtime.h>
@@ -34,8 +39,6 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kPrefixDw = 24;      // 96-byte header prefix
 constexpr int kFastDw = 16;        // the fast shape needs 64 bytes
 constexpr int kStreamBase = 96;    // long segments: streamed from here
-constexpr int kGroup = 16;         // lanes per packet in the streaming sum
-constexpr int kStreamUnroll = 8;   // 16-byte loads per lane per pass
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));  // frames are 4-byte aligned

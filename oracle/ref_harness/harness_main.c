@@ -28,6 +28,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "../../include/ixgrx.h"
 #include "ref_capture.h"
@@ -269,8 +270,16 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 
 int main(int argc, char **argv)
 {
+	/* -t SECONDS: after the run, repeat it until SECONDS have passed and
+	 * print the 1-core rate (bench.py's "reference" CPU figure) */
+	double tsec = 0;
+	if (argc == 5 && !strcmp(argv[1], "-t")) {
+		tsec = atof(argv[2]);
+		argv += 2;
+		argc -= 2;
+	}
 	if (argc != 3) {
-		fprintf(stderr, "usage: ixref_rx IN OUT\n");
+		fprintf(stderr, "usage: ixref_rx [-t SECONDS] IN OUT\n");
 		return 1;
 	}
 	FILE *fi = fopen(argv[1], "rb");
@@ -315,5 +324,20 @@ int main(int argc, char **argv)
 	fwrite(recs, sizeof(*recs), n, fo);
 	fwrite(cs, 4, n, fo);
 	fclose(fo);
+	if (tsec > 0 && n > 0) {
+		struct timespec t0, t1;
+		uint64_t done = 0;
+		double el = 0;
+		clock_gettime(CLOCK_MONOTONIC, &t0);
+		do {
+			for (uint32_t i = 0; i < n; i++)
+				one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], i);
+			done += n;
+			clock_gettime(CLOCK_MONOTONIC, &t1);
+			el = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+		} while (el < tsec);
+		printf("{\"pkts\": %llu, \"seconds\": %.6f, \"ns_per_pkt\": %.3f}\n",
+		       (unsigned long long)done, el, 1e9 * el / (double)done);
+	}
 	return 0;
 }

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round profile on the GPU box (run through gpurun from the repo root):
+#   1. rocprofv3 --kernel-trace --stats of the default bench command
+#   2. --pmc FETCH_SIZE and --pmc WRITE_SIZE passes per workload (separate
+#      runs, kernel-trace only; no sys/runtime traces with --pmc)
+#   3. traffic.json from the PMC passes, then the plain bench line
+# Everything lands in gpurun_out/$TAG; summaries are copied into profiles/
+# by hand afterwards.
+TAG=${1:-r01}
+O=gpurun_out/$TAG
+mkdir -p "$O"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+B="bench.py --steps 20 --warmup 5"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- python3 $B \
+  > "$O/bench_under_rocprof.json" 2> "$O/kt.log" || { echo "kernel-trace run failed"; tail -20 "$O/kt.log"; exit 1; }
+du -sh "$O"/* ; find "$O" -size +1M -exec ls -la {} \;
+SPECS=""
+for W in c2 c4 c3 c5; do
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_${W}_$C" -o p -- python3 bench.py --workload $W \
+      --secondary '' --no-cpu --no-copy --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
+      || { echo "pmc $W $C failed"; tail -20 "$O/pmc_${W}_$C.log"; exit 1; }
+    find "$O/pmc_${W}_$C" -type f -exec ls -la {} \;
+    [ -n "$(find "$O/pmc_${W}_$C" -name '*counter_collection.csv')" ] || { echo "no csv: $W $C"; tail -30 "$O/pmc_${W}_$C.log"; find "$O" -size +1M -delete; exit 1; }
+  done
+  SPECS="$SPECS $W:$O/pmc_${W}_FETCH_SIZE:$O/pmc_${W}_WRITE_SIZE"
+done
+find "$O" -size +8M -exec ls -la {} \; -delete
+python3 tools/pmc_traffic.py "$O/traffic.json" $SPECS || exit 1
+mkdir -p profiles && cp "$O/traffic.json" profiles/traffic.json
+timeout -k 10 400 python3 $B > "$O/bench.json" 2> "$O/bench.log" || { echo "bench failed"; tail -20 "$O/bench.log"; exit 1; }
+cat "$O/bench.json"
