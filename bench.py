@@ -130,9 +130,8 @@ def time_steps(wl, eng, steps, warmup, dist, world):
     el = time.perf_counter() - t0
     kern = [a.elapsed_time(b) * 1e-3 for a, b in ev]
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        from ix_amd.shard import max_over_ranks
+        el = max_over_ranks(el, dist, device="cuda")
     return el, float(np.mean(kern)), float(np.min(kern))
 
 

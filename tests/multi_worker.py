@@ -1,0 +1,49 @@
+"""One rank of tests/test_multi.py (launched as a subprocess per rank).
+
+env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT, IXT_KIND, IXT_N,
+IXT_ENGINE ("oracle": CPU stand-in for the per-rank device call, tests only;
+"hip": the product engine on cuda:0).
+Every rank checks the gathered records against the oracle over the whole
+batch and exits 0 on success.
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from ix_amd import shard, traces  # noqa: E402
+from oracle import oracle  # noqa: E402
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    kind, n, eng = os.environ["IXT_KIND"], int(os.environ["IXT_N"]), os.environ["IXT_ENGINE"]
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    flags = 2 if kind == "mixed" else 0
+    tr = traces.make_trace(kind, n, seed=77, bad_ip=0.02, bad_l4=0.02)
+    bounds = shard.shard_bounds(tr.len, world)
+    s, e = bounds[rank]
+    part = shard.shard_trace(tr, s, e)
+    if eng == "hip":
+        from ix_amd import ixgrx
+        rec = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, 128, 0, flags), device=0).batch_trace(part)
+        rec = rec.view(np.uint8).reshape(-1, 16)
+    else:
+        rec, _ = oracle.rx_trace(part, traces.RSS_KEY, flags=flags)
+    allrec = shard.gather_records(rec, bounds, dist)
+    exp, _ = oracle.rx_trace(tr, traces.RSS_KEY, flags=flags)
+    ok = allrec.shape == exp.shape and bool((allrec == exp).all())
+    slowest = shard.max_over_ranks(float(rank + 1), dist)
+    ok = ok and slowest == float(world)
+    dist.barrier()
+    dist.destroy_process_group()
+    print(f"rank {rank}: slice [{s},{e}) ok={ok}", flush=True)
+    sys.exit(0 if ok else 1)
+
+
+if __name__ == "__main__":
+    main()

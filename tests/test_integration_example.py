@@ -1,0 +1,34 @@
+"""examples/ix_rx_shim.c (INTEGRATION.md's call-site sketch) builds against
+include/ixgrx.h + libixgrx.so and runs: on CPU it must fail cleanly at
+ixg_rx_init (no device, exit 2); on the GPU all 64 frames reach the TCP
+callee."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _build(tmp_path):
+    exe = str(tmp_path / "ix_rx_shim")
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", "-I" + os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "ix_rx_shim.c"), "-L" + os.path.join(ROOT, "ix_amd"),
+                    "-lixgrx", "-Wl,-rpath," + os.path.join(ROOT, "ix_amd"), "-o", exe], check=True)
+    return exe
+
+
+def test_example_builds_and_fails_cleanly_without_gpu(tmp_path):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu test")
+    r = subprocess.run([_build(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stdout + r.stderr
+    assert "ixg_rx_init" in r.stderr
+
+
+@pytest.mark.gpu
+def test_example_runs_on_gpu(tmp_path):
+    r = subprocess.run([_build(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "tcp=64" in r.stdout

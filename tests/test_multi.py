@@ -1,0 +1,81 @@
+"""N>1 path: byte-balanced sharding, per-rank processing, record gather and
+the max-over-ranks timing rule, with world_size 2 over gloo.
+Each rank is a separate process (tests/multi_worker.py), as under torchrun."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from ix_amd import shard, traces
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, kind, n, engine, timeout=300):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), IXT_KIND=kind, IXT_N=str(n), IXT_ENGINE=engine)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "multi_worker.py")], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out))
+    for rc, out in outs:
+        assert rc == 0, out[-2000:]
+
+
+@pytest.mark.parametrize("kind,n", [("imix", 3001), ("tcp64", 4096), ("mixed", 2000)])
+def test_two_ranks_gloo(kind, n):
+    _run(2, kind, n, "oracle")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n", [("imix", 20001), ("mixed", 20000)])
+def test_two_ranks_gloo_hip(kind, n):
+    """Both ranks drive the HIP engine on the box's one GPU."""
+    _run(2, kind, n, "hip")
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_bounds_balanced(world):
+    tr = traces.make_trace("imix", 5000, seed=3)
+    b = shard.shard_bounds(tr.len, world)
+    assert b[0][0] == 0 and b[-1][1] == tr.n
+    assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+    w = (tr.len.astype(np.int64) + 3) & ~3
+    sizes = [int(w[s:e].sum()) for s, e in b]
+    assert max(sizes) - min(sizes) <= 2 * 1516
+
+
+def test_shard_bounds_small():
+    assert shard.shard_bounds(np.zeros(0, np.uint16), 4) == [(0, 0)] * 4
+    b = shard.shard_bounds(np.array([60], np.uint16), 2)
+    assert sorted(e - s for s, e in b) == [0, 1]
+
+
+def test_shard_trace_frames_identical():
+    for kind in ("imix", "tcp64"):
+        tr = traces.make_trace(kind, 777, seed=9)
+        for s, e in shard.shard_bounds(tr.len, 3):
+            part = shard.shard_trace(tr, s, e)
+            assert part.n == e - s
+            for i in (0, part.n // 2, part.n - 1):
+                assert part.frame(i) == tr.frame(s + i)
+            assert part.blob.shape[0] >= int(part.offsets()[-1]) + int(part.len[-1]) + traces.TAIL_PAD
