@@ -19,8 +19,7 @@ struct ixg_ctx {
 	int device;
 	struct ixg_rx_cfg cfg;
 	uint32_t crc_const;
-	uint32_t grid_fast;  /* persistent grids: CUs x resident blocks per CU */
-	uint32_t grid_gen;
+	uint32_t ncu;        /* compute units: persistent grids are sized from it */
 	int force_general;   /* IXGRX_FORCE_GENERAL=1: skip the fixed-shape kernel (tests/A-B) */
 	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
 	uint8_t *d_defer;    /* one flag per 64-packet chunk */
@@ -191,8 +190,7 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		e = getenv("IXGRX_GEN_VARIANT");
 		c->fast_variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
 	}
-	c->grid_fast = (uint32_t)prop.multiProcessorCount * (uint32_t)ixgrx_blocks_per_cu(c->fast_variant & 0xff);
-	c->grid_gen = (uint32_t)prop.multiProcessorCount * (uint32_t)ixgrx_blocks_per_cu(-1 - ((c->fast_variant >> 8) & 0xff));
+	c->ncu = (uint32_t)prop.multiProcessorCount;
 	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
 	if (!tab) {
 		rc = -ENOMEM;
@@ -265,16 +263,7 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 		}
 		p.defer = c->d_defer;
 	}
-	uint32_t blk = ixgrx_block();
-	uint64_t want_f = (nchunks + blk / 64 - 1) / (blk / 64);     /* one wave per chunk */
-	uint64_t want_g = (((nchunks + 63) / 64) + blk / 64 - 1) / (blk / 64); /* one wave per 64 chunks */
-	uint32_t gf = want_f < c->grid_fast ? (uint32_t)want_f : c->grid_fast;
-	uint32_t gg = want_g < c->grid_gen ? (uint32_t)want_g : c->grid_gen;
-	if (gf == 0)
-		gf = 1;
-	if (gg == 0)
-		gg = 1;
-	return ixgrx_launch(&p, c->fast_variant, gf, gg, s) == 0 ? 0 : -EIO;
+	return ixgrx_launch(&p, c->fast_variant, c->ncu, s) == 0 ? 0 : -EIO;
 }
 
 int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,

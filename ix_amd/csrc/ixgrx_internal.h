@@ -36,10 +36,12 @@ typedef struct ixg_kparams ixg_kparams;
 #define IXG_ZERO_PAGE 4096u
 
 /* implemented in ixgrx_kernels.hip */
-int ixgrx_launch(const void *params, int fast_variant, uint32_t grid_fast, uint32_t grid_gen, void *stream);
+/* enqueue one batch: the fixed-shape kernel (when p->defer) and the general
+ * kernel; grids are sized from the device's CU count and each kernel's
+ * occupancy */
+int ixgrx_launch(const void *params, int variant, uint32_t ncu, void *stream);
 uint32_t ixgrx_kparams_size(void);
 uint32_t ixgrx_block(void);
-int ixgrx_blocks_per_cu(int which); /* >= 0: fixed-shape kernel variant k, < 0: general variant -1-which */
 
 #ifdef __cplusplus
 }

@@ -194,3 +194,45 @@ def test_full_size_1514_tiled(engines):
     torch.cuda.synchronize()
     exp = torch.from_numpy(er).to(dev).repeat(n // pool, 1)
     assert torch.equal(out, exp)
+
+
+@pytest.mark.parametrize("S", [4, 16, 32, 48, 60, 64])
+def test_fixed_strides_up_to_64(S, engines):
+    """The coalesced fixed-shape path (stride <= 64): valid 60 B frames where
+    they fit the slot, plus random bytes and lengths 0..64 (frames longer
+    than the stride overlap the next slot), ragged last chunk."""
+    rng = np.random.default_rng(S)
+    n = 64 * 37 + 13
+    blob = rng.integers(0, 256, n * S + 64 + 64, dtype=np.uint8)
+    lens = rng.integers(0, 65, n).astype(np.uint16)
+    if S >= 60:
+        rows = traces.build_ipv4(rng, n, 60, 6)
+        good = rng.random(n) < 0.8
+        for i in np.nonzero(good)[0]:
+            blob[i * S:i * S + 60] = rows[i]
+            lens[i] = 60
+    for flags in (0, ixgrx.IXG_F_NO_CSUM_DROP):
+        rec, cs = engines(flags=flags).batch_host(blob, None, lens, S, want_csum=True)
+        er, ec = oracle.rx_batch(KEY, 128, 0, flags, blob, None, lens, S)
+        _diff(rec, er, f"stride {S}")
+        assert (cs == ec).all()
+
+
+def test_fixed_stride_all_fast_and_misaligned_base(engines):
+    """A batch whose chunks are all fixed-shape, at a 16-B aligned base
+    (coalesced kernel) and at a base 4 bytes off (lane-load kernel)."""
+    import torch
+    tr = traces.make_trace("tcp64", 64 * 500 + 7, seed=12, bad_ip=0.01, bad_l4=0.01)
+    er, ec = oracle.rx_trace(tr, KEY, threads=8)
+    dev = torch.device("cuda:0")
+    for shift in (0, 4):
+        raw = torch.zeros(tr.blob.shape[0] + 64, dtype=torch.uint8, device=dev)
+        raw[shift:shift + tr.blob.shape[0]] = torch.from_numpy(tr.blob).to(dev)
+        lens = torch.from_numpy(tr.len.astype(np.int16)).to(dev)
+        out = torch.empty((tr.n, 16), dtype=torch.uint8, device=dev)
+        cs = torch.empty(tr.n, dtype=torch.int32, device=dev)
+        engines().batch_dev(raw.data_ptr() + shift, None, lens.data_ptr(), tr.stride, tr.n, out.data_ptr(),
+                            cs.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        _diff(out.cpu().numpy(), er, f"shift {shift}")
+        assert (cs.cpu().numpy().view(np.uint32) == ec).all()
