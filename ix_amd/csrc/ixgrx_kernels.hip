@@ -65,6 +65,57 @@ DEV uint32_t add1c(uint32_t a, uint32_t b) {
 
 DEV uint32_t fold32(uint64_t s) { return add1c((uint32_t)s, (uint32_t)(s >> 32)); }
 
+// acc + a + b (8 dwords) in one's complement (end-around carry) arithmetic:
+// one v_add/v_addc per dword and one to fold the last carry. Only additions:
+// the result is 0 only if acc and every dword are 0 (the representation
+// chksum_internet produces). The final carry-in cannot overflow: after an
+// add that carried out, the partial sum is <= 0xfffffffe.
+// Two independent adc8 chains interleaved (carries in VCC and in an SGPR
+// pair), so consecutive instructions do not depend on each other.
+DEV void adc8x2(uint32_t& acc0, const u32x4& a, const u32x4& b, uint32_t& acc1, const u32x4& c, const u32x4& d) {
+  uint64_t cc;
+  asm volatile(
+      "v_add_co_u32 %0, vcc, %0, %3\n\t"
+      "v_add_co_u32 %1, %2, %1, %11\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %4, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %12, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %5, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %13, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %6, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %14, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %7, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %15, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %8, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %16, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %9, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %17, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %10, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, %18, %2\n\t"
+      "v_addc_co_u32 %0, vcc, %0, 0, vcc\n\t"
+      "v_addc_co_u32 %1, %2, %1, 0, %2"
+      : "+v"(acc0), "+v"(acc1), "=&s"(cc)
+      : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w),
+        "v"(c.x), "v"(c.y), "v"(c.z), "v"(c.w), "v"(d.x), "v"(d.y), "v"(d.z), "v"(d.w)
+      : "vcc");
+}
+
+DEV uint32_t adc8(uint32_t acc, const u32x4& a, const u32x4& b) {
+  asm volatile(
+      "v_add_co_u32 %0, vcc, %0, %1\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %2, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %3, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %4, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %5, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %6, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %7, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %8, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, 0, vcc"
+      : "+v"(acc)
+      : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w), "v"(b.x), "v"(b.y), "v"(b.z), "v"(b.w)
+      : "vcc");
+  return acc;
+}
+
 // mask of the first k bytes of a dword, k in [0, 4]
 DEV uint32_t ones(int k) { return k >= 4 ? 0xffffffffu : ((1u << (8 * k)) - 1u); }
 
@@ -429,7 +480,7 @@ constexpr int kT = 8;
 
 struct WaveLds {  // per-wave scratch, LDS address space
   lds_u32* list;  // compacted long lanes
-  lds_u32* end;   // per lane: segment end
+  lds_u32* end;   // per lane: end of the whole 16-byte pieces to stream
   lds_u32* offlo; // per lane: frame offset (low/high words)
   lds_u32* offhi;
   lds_u32* sum;   // per lane: streamed tail sum
@@ -437,7 +488,7 @@ struct WaveLds {  // per-wave scratch, LDS address space
 
 struct Round {
   u32x4 v[kT];
-  uint32_t end;   // owner's segment end (0: this group has no packet)
+  uint32_t end;   // owner's end of whole pieces (0: this group has no packet)
   uint32_t owner;
 };
 
@@ -459,41 +510,25 @@ DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, uint32_t nl
   }
 }
 
-// b.v[t] for a per-lane t in [0, kT): binary mux on the bits of t (a ?:
-// chain indexed by t would be turned back into a scratch-memory access)
-DEV u32x4 pick_piece(const u32x4 (&v)[kT], uint32_t t) {
-  static_assert(kT == 8, "3-level mux");
-  const bool b0 = t & 1u, b1 = t & 2u, b2 = t & 4u;
-  const u32x4 a0 = b0 ? v[1] : v[0], a1 = b0 ? v[3] : v[2], a2 = b0 ? v[5] : v[4], a3 = b0 ? v[7] : v[6];
-  const u32x4 c0 = b1 ? a1 : a0, c1 = b1 ? a3 : a2;
-  return b2 ? c1 : c0;
-}
-
 DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round& b) {
   const int gl = lane % kG;
-  // every piece is either inside the segment or zero: plain 32-bit word sum
-  uint64_t acc = 0;
+  // every piece is inside the segment or reads the zero page (pass A summed
+  // the piece holding the segment end, masked): plain one's complement sums
+  static_assert(kT % 4 == 0, "two interleaved chains of piece pairs");
+  uint32_t a = 0, a1 = 0;
 #pragma unroll
-  for (int t = 0; t < kT; t++) acc += (uint64_t)b.v[t].x + b.v[t].y + b.v[t].z + b.v[t].w;
-  // except the one piece that straddles the end: take back its bytes >= end
-  const int rem0 = (int)b.end - (int)(kStreamBase + 16u * gl);
-  const uint32_t r = (uint32_t)rem0 & 255u, tb = (uint32_t)rem0 >> 8;
-  if (rem0 > 0 && r != 0u && r < 16u && tb < (uint32_t)kT) {
-    const u32x4 vb = pick_piece(b.v, tb);
-    const int ri = (int)r;
-    acc -= (uint64_t)(vb.x & ~ones(ri)) + (vb.y & ~ones(ri - 4 < 0 ? 0 : ri - 4)) +
-           (vb.z & ~ones(ri - 8 < 0 ? 0 : ri - 8)) + (vb.w & ~ones(ri - 12 < 0 ? 0 : ri - 12));
-  }
-  uint32_t a = fold32(acc);
+  for (int t = 0; t < kT; t += 4) adc8x2(a, b.v[t], b.v[t + 1], a1, b.v[t + 2], b.v[t + 3]);
+  a = add1c(a, a1);
   // frames longer than 96 + 2 KiB (not IX mbufs): the rest, synchronously
   const uint32_t more = kStreamBase + 16u * kG * kT;
   if (__any(b.end > more)) {
     const uint64_t off = ((uint64_t)w.offhi[b.owner] << 32) | w.offlo[b.owner];
     const uint8_t* zero = p.zero + 16 * lane;
-    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 16u * kG) {
+    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 32u * kG) {
       const uint32_t pos = pos0 + 16u * gl;
-      const u32x4 v = load16(pos < b.end, p.base + off + pos, zero);
-      a = add1c(a, fold32(piece_sum(v, (int)b.end - (int)pos)));
+      const u32x4 v0 = load16(pos < b.end, p.base + off + pos, zero);
+      const u32x4 v1 = load16(pos + 16u * kG < b.end, p.base + off + pos + 16u * kG, zero);
+      a = adc8(a, v0, v1);
     }
   }
 #pragma unroll
@@ -511,13 +546,27 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   const uint64_t off = frame_off<OFFS>(p, ic);
   uint32_t d[kPrefixDw];
   load_prefix<0, 6>(p.base + off, L, reinterpret_cast<const uint8_t*>(p.tab), d);
+  // bytes 96..111 of frames shorter than 128 B, issued with the prefix: the
+  // end piece of their segment (no dependent load for those)
+  const bool short_tail = L > (uint32_t)kStreamBase && L < (uint32_t)kStreamBase + 32u;
+  u32x4 v96 = {0u, 0u, 0u, 0u};
+  if (__any(short_tail)) v96 = load16(short_tail, p.base + off + kStreamBase, p.zero + 16 * lane);
   LaneState s;
   const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
   if (__all(fixed))
     lane_parse<true, kPrefixDw>(p, T, d, L, s);
   else
     lane_parse<false, kPrefixDw>(p, T, d, L, s);
-  const bool lng = valid && s.stream;
+  // The 16-byte piece (counted from byte 96) holding the segment end is
+  // summed by this lane, masked to the segment; streaming rounds read only
+  // the whole pieces before it. A segment ending within 16 bytes past the
+  // prefix is finished with v96; a longer one loads its end piece now and
+  // adds it after the rounds, so the load's latency hides behind them.
+  const bool strm = valid && s.stream;
+  const uint32_t tail = s.seg_end - (uint32_t)kStreamBase;
+  const uint32_t rr = tail & 15u, pend = (uint32_t)kStreamBase + (tail & ~15u);
+  const bool lng = strm && (pend > (uint32_t)kStreamBase || !short_tail);
+  if (strm && !lng) s.l4_acc += piece_sum(v96, (int)rr);
   const uint64_t m = __ballot(lng);
   if (!m) {  // no long segment in this chunk (wave-uniform)
     if (valid) {
@@ -532,6 +581,7 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   Rec rok = make_record(p, d, L, s, r4);
   Rec rbad = make_record(p, d, L, s, 1u);
   uint32_t acc32 = fold32(s.l4_acc), ip_res = s.ip_res;
+  const u32x4 ve = load16(lng && rr != 0u, p.base + off + pend, p.zero + 16 * lane);
   // materialise these now, so the parse state (d[], s) is dead during the
   // streaming rounds instead of being kept live for sunk computations
   asm volatile("" : "+v"(rok.w0), "+v"(rok.w1), "+v"(rok.w2), "+v"(rok.w3));
@@ -539,7 +589,7 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   asm volatile("" : "+v"(acc32), "+v"(ip_res));
   if (lng) {
     w.list[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)lane;
-    w.end[lane] = s.seg_end;
+    w.end[lane] = pend;
     w.offlo[lane] = (uint32_t)off;
     w.offhi[lane] = (uint32_t)(off >> 32);
   }
@@ -558,7 +608,8 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   __builtin_amdgcn_wave_barrier();
   if (valid) {
     if (lng) {
-      const uint32_t res = (~fold16(add1c(acc32, w.sum[lane]))) & 0xffffu;
+      const uint32_t end_piece = fold32(piece_sum(ve, (int)rr));
+      const uint32_t res = (~fold16(add1c(add1c(acc32, w.sum[lane]), end_piece))) & 0xffffu;
       store_record(p, i, res == 0 ? rok : rbad, ip_res, res);
     } else {
       store_record(p, i, rok, ip_res, r4);
@@ -833,10 +884,16 @@ DEV void general_body(const KParams& p) {
   }
 }
 
-#define IXG_GEN_KERNEL(NAME, OFFS) \
-  extern "C" __global__ void __launch_bounds__(kBlock) NAME(KParams p) { general_body<OFFS>(p); }
-IXG_GEN_KERNEL(ixg_rx_general_s, false)
-IXG_GEN_KERNEL(ixg_rx_general_o, true)
+#define IXG_GEN_KERNEL(NAME, OFFS, WAVES)                                                           \
+  extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
+  NAME(KParams p) { general_body<OFFS>(p); }
+// variants for A/B (IXGRX_GEN_VARIANT); index 0 is the default
+IXG_GEN_KERNEL(ixg_rx_general_s, false, 2)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, 2)
+IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, 3)
+IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, 3)
+IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, 4)
+IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, 4)
 
 typedef void (*kern_fn)(KParams);
 // [variant][layout: 0 = stride, 1 = offsets]
@@ -844,7 +901,9 @@ static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
                                     {ixg_rx_fast_a2w4_s, ixg_rx_fast_a2w4_o},
                                     {ixg_rx_fast_a2w5_s, ixg_rx_fast_a2w5_o},
                                     {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}};
-static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o}};
+static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
+                                   {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
+                                   {ixg_rx_general_w4_s, ixg_rx_general_w4_o}};
 static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
 static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
 

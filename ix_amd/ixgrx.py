@@ -77,14 +77,15 @@ class Config:
         return c
 
 
-_lib = None
+_libs: dict[str, ctypes.CDLL] = {}
 
 
 def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load libixgrx.so; raises if it has not been built (no silent fallback)."""
-    global _lib
-    if _lib is not None:
-        return _lib
+    """Load libixgrx.so (or another build of it, for A/B timing); raises if
+    it has not been built (no silent fallback)."""
+    path = os.path.abspath(path)
+    if path in _libs:
+        return _libs[path]
     if not os.path.exists(path):
         raise RuntimeError(f"{path} missing: build it with __graft_entry__.build() "
                            "(make -C ix_amd/csrc)")
@@ -119,13 +120,13 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_dispatch.restype = u32
     if lib.ixg_abi_version() != ABI_VERSION:
         raise RuntimeError("libixgrx ABI version mismatch")
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
-def _check(rc: int, what: str) -> None:
+def _check(rc: int, what: str, lib: ctypes.CDLL | None = None) -> None:
     if rc != 0:
-        msg = load_library().ixg_strerror(rc).decode()
+        msg = (lib or load_library()).ixg_strerror(rc).decode()
         raise RuntimeError(f"{what} failed: {rc} ({msg})")
 
 
@@ -141,19 +142,21 @@ def hash_tables(cfg: Config) -> tuple[np.ndarray, int]:
 
 @dataclass
 class RxEngine:
-    """One ixg_rx context on HIP device `device`."""
+    """One ixg_rx context on HIP device `device` (lib_path: another build of
+    the library, for A/B timing; default ix_amd/libixgrx.so)."""
     cfg: Config
     device: int = 0
+    lib_path: str = LIB_PATH
     _ctx: ctypes.c_void_p = field(default_factory=ctypes.c_void_p, init=False)
 
     def __post_init__(self):
-        lib = load_library()
+        self._lib = lib = load_library(self.lib_path)
         self._ccfg = self.cfg.to_c()
-        _check(lib.ixg_rx_init(ctypes.byref(self._ccfg), self.device, ctypes.byref(self._ctx)), "ixg_rx_init")
+        _check(lib.ixg_rx_init(ctypes.byref(self._ccfg), self.device, ctypes.byref(self._ctx)), "ixg_rx_init", lib)
 
     def close(self) -> None:
         if self._ctx:
-            load_library().ixg_rx_fini(self._ctx)
+            self._lib.ixg_rx_fini(self._ctx)
             self._ctx = ctypes.c_void_p()
 
     def __del__(self):
@@ -166,8 +169,8 @@ class RxEngine:
                   csum: int | None = None, stream: int | None = None) -> None:
         """Device-resident batch: all arguments are device pointers (ints)."""
         fr = RxFrames(base, off or None, length, stride, 0)
-        _check(load_library().ixg_rx_batch_dev(self._ctx, ctypes.byref(fr), n, out, csum or None,
-                                               stream or None), "ixg_rx_batch_dev")
+        _check(self._lib.ixg_rx_batch_dev(self._ctx, ctypes.byref(fr), n, out, csum or None,
+                                          stream or None), "ixg_rx_batch_dev", self._lib)
 
     def batch_host(self, blob: np.ndarray, off: np.ndarray | None, lens: np.ndarray, stride: int = 0,
                    want_csum: bool = False):
@@ -178,9 +181,9 @@ class RxEngine:
         offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
         rec = np.zeros(n, dtype=REC_DTYPE)
         cs = np.zeros(n, dtype=np.uint32) if want_csum else None
-        _check(load_library().ixg_rx_batch_host(
+        _check(self._lib.ixg_rx_batch_host(
             self._ctx, blob.ctypes.data, None if offa is None else offa.ctypes.data, lens.ctypes.data,
-            stride, n, rec.ctypes.data, None if cs is None else cs.ctypes.data), "ixg_rx_batch_host")
+            stride, n, rec.ctypes.data, None if cs is None else cs.ctypes.data), "ixg_rx_batch_host", self._lib)
         return (rec, cs) if want_csum else rec
 
     def batch_trace(self, tr, want_csum: bool = False):
@@ -191,8 +194,8 @@ class RxEngine:
         ptrs = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
         n = int(ptrs.shape[0])
         rec = np.zeros(n, dtype=REC_DTYPE)
-        _check(load_library().ixg_rx_batch_mbufs(self._ctx, ptrs.ctypes.data, n, rec.ctypes.data),
-               "ixg_rx_batch_mbufs")
+        _check(self._lib.ixg_rx_batch_mbufs(self._ctx, ptrs.ctypes.data, n, rec.ctypes.data),
+               "ixg_rx_batch_mbufs", self._lib)
         return rec
 
 

@@ -236,3 +236,21 @@ def test_fixed_stride_all_fast_and_misaligned_base(engines):
         torch.cuda.synchronize()
         _diff(out.cpu().numpy(), er, f"shift {shift}")
         assert (cs.cpu().numpy().view(np.uint32) == ec).all()
+
+
+def test_jumbo_frames(engines):
+    """Segments far past one streaming round (96 + 2 KiB): jumbo TCP/UDP
+    frames of odd and even lengths, some with bad checksums."""
+    rng = np.random.default_rng(77)
+    frames = []
+    for L in (2143, 2144, 2145, 2160, 3001, 4096, 9014, 16000, 30001, 65000):
+        for proto in (6, 17):
+            rows = traces.build_ipv4(rng, 3, L, proto)
+            traces.corrupt(rng, rows, 0.0, 0.34, 34 + (16 if proto == 6 else 6))
+            frames += [bytes(r) for r in rows]
+    tr = traces.pack(frames)
+    for flags in (0, ixgrx.IXG_F_NO_CSUM_DROP):
+        rec, cs = engines(flags=flags).batch_trace(tr, want_csum=True)
+        er, ec = oracle.rx_trace(tr, KEY, flags=flags)
+        _diff(rec, er, "jumbo")
+        assert (cs == ec).all()

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Interleaved A/B of kernel builds in ONE process (guide rule 24).
+"""Interleaved A/B of library BUILDS in one process: the working tree's
+ix_amd/libixgrx.so against builds of other revisions (tools/build_rev.sh).
+Box-to-box variance on the pool is larger than most kernel changes, so a
+change is judged only against a reference timed in the same process.
 
-Creates one engine per IXGRX_FAST_VARIANT (plus the general-only path),
-runs R rounds x K launches each, round-robin over the variants, and prints
-median/min per-launch milliseconds per variant (events around each launch).
+usage: ab_lib.py --workload c4 --libs ix_amd/libixgrx.so,tools/ablib/base.so [--general]
 """
 import argparse
 import json
@@ -19,33 +20,29 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c2")
-    ap.add_argument("--variants", default="0,1,2,3,g")
+    ap.add_argument("--libs", required=True)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--general", action="store_true", help="IXGRX_FORCE_GENERAL=1 for every build")
     args = ap.parse_args()
     import torch
     import bench
     from ix_amd import ixgrx, traces
     dev = torch.device("cuda:0")
-    wl = bench.Workload(args.workload, seed=0x1B0002, dev=dev, n=args.n)
+    wl = bench.Workload(args.workload, seed=0x1B0002, dev=dev)
+    os.environ["IXGRX_FORCE_GENERAL"] = "1" if args.general else "0"
     engs = {}
-    for v in args.variants.split(","):
-        # "3" = fast variant 3; "0:1" = fast variant 0 + general variant 1;
-        # "g1" = general-only with general variant 1
-        os.environ["IXGRX_FORCE_GENERAL"] = "1" if v.startswith("g") else "0"
-        fv, _, gv = (("0", "", v[1:] or "0") if v.startswith("g") else v.partition(":"))
-        os.environ["IXGRX_FAST_VARIANT"] = fv
-        os.environ["IXGRX_GEN_VARIANT"] = gv or "0"
-        engs[v] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags))
+    for path in args.libs.split(","):
+        engs[os.path.basename(path)] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags),
+                                                      lib_path=os.path.join(ROOT, path))
     s = torch.cuda.current_stream()
-    times = {v: [] for v in engs}
     ok = {}
-    for v, e in engs.items():  # warm + parity
+    for v, e in engs.items():
         for _ in range(3):
             wl.launch(e, s.cuda_stream)
         torch.cuda.synchronize()
         ok[v] = wl.check(traces.RSS_KEY)
+    times = {v: [] for v in engs}
     for _ in range(args.rounds):
         for v, e in engs.items():
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.k)]
@@ -59,9 +56,8 @@ def main():
     for v, t in times.items():
         t = np.array(t)
         res[v] = {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(t.min()), 4),
-                  "gpkt_s": round(wl.n / np.median(t) / 1e6, 2),
                   "frac": round(wl.bytes_per_pkt * wl.n / (np.median(t) * 1e-3) / 8e12, 4), "parity": ok[v]}
-    print(json.dumps({"workload": args.workload, "n": wl.n, "results": res}))
+    print(json.dumps({"workload": args.workload, "general_only": args.general, "results": res}))
 
 
 if __name__ == "__main__":
