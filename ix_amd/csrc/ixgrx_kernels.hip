@@ -186,9 +186,11 @@ struct LaneState {
 // FIXED: every lane is IPv4 with ihl 5 (wave-uniform), so the header
 // geometry is constant-folded. NDW: prefix dwords available; a segment
 // ending past 4*NDW bytes is left to the streaming rounds.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
 template <bool FIXED, int NDW>
 DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint32_t (&d)[kPrefixDw],
-                    uint32_t L, LaneState& s) {
+                    uint32_t L, LaneState& s, const lds_u32* T6 = nullptr) {
   const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);       // ip.c:132
   const uint32_t vh = byte_at(d, 14);
   const uint32_t ver = vh >> 4;
@@ -259,14 +261,14 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
     s.rss = (uint32_t)hx;
     s.flags |= IXG_RF_RSS;
   }
-  // IPv6 extension: Toeplitz over src(16) dst(16) sport dport from a global
-  // 36 x 256 table (L2-resident; only v6 lanes touch it)
+  // IPv6 extension: Toeplitz over src(16) dst(16) sport dport from the
+  // 36 x 256 table, staged in LDS by the general kernel
   if (v6 && L >= 58 && ver == 6 && (s.proto == 6 || s.proto == 17)) {
     uint32_t h = 0;
 #pragma unroll
-    for (int k = 0; k < 32; k++) h ^= p.tab6[(k << 8) | byte_at(d, 22 + k)];
+    for (int k = 0; k < 32; k++) h ^= T6[(k << 8) | byte_at(d, 22 + k)];
 #pragma unroll
-    for (int k = 0; k < 4; k++) h ^= p.tab6[((32 + k) << 8) | byte_at(d, 54 + k)];
+    for (int k = 0; k < 4; k++) h ^= T6[((32 + k) << 8) | byte_at(d, 54 + k)];
     s.rss = h;
     s.flags |= IXG_RF_RSS;
   }
@@ -456,7 +458,6 @@ DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t
 // LDS (address space 3) pointers: through generic pointers these would be
 // flat_* accesses, which count on vmcnt as well and force vmcnt(0) waits
 // that serialise the streaming loads.
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
 #define LDS(T, x) ((T*)(x))
 
 // masked sum of a 16-byte piece whose first byte is `rem` bytes before the
@@ -477,6 +478,7 @@ DEV uint64_t piece_sum(const u32x4& v, int rem) {
 constexpr int kG = 16;
 constexpr int kRoundPk = 64 / kG;
 constexpr int kT = 8;
+constexpr int kQGroups = 4;  // groups of 64 chunks per wave per chunk-list fill
 
 struct WaveLds {  // per-wave scratch, LDS address space
   lds_u32* list;  // compacted long lanes
@@ -484,6 +486,7 @@ struct WaveLds {  // per-wave scratch, LDS address space
   lds_u32* offlo; // per lane: frame offset (low/high words)
   lds_u32* offhi;
   lds_u32* sum;   // per lane: streamed tail sum
+  const lds_u32* t6;  // IPv6 Toeplitz table (IXG_F_IPV6), block-shared
 };
 
 struct Round {
@@ -536,27 +539,52 @@ DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round&
   if (gl == 0 && b.end != 0u) w.sum[b.owner] = a;
 }
 
+// A chunk's descriptors and frame bytes, loaded ahead by general_body's
+// pipeline (descriptors two chunks ahead, bytes one chunk ahead).
+struct GDesc {
+  uint32_t L;
+  uint64_t off;
+};
+struct GPre {
+  uint32_t d[kPrefixDw];  // bytes 0..95 (0..11 never loaded), zero past L
+  u32x4 v96;              // bytes 96..111 of frames shorter than 128 B, else zero page
+};
+
+constexpr uint32_t kNoChunk = 0xffffffffu;
+
+template <bool OFFS>
+DEV void gen_desc(const KParams& p, uint32_t chunk, int lane, GDesc& g) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = chunk != kNoChunk && i < p.n;
+  const uint32_t ic = valid ? i : 0u;  // clamped: descriptor loads without a branch
+  g.L = valid ? (uint32_t)p.len[ic] : 0u;
+  g.off = frame_off<OFFS>(p, ic);
+}
+
+// every load is issued (zero page / dummy when there is nothing to read), so
+// hipcc's vmcnt accounting stays exact across the pipeline
+DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
+  load_prefix<0, 6>(p.base + g.off, g.L, reinterpret_cast<const uint8_t*>(p.tab), x.d);
+  const bool short_tail = g.L > (uint32_t)kStreamBase && g.L < (uint32_t)kStreamBase + 32u;
+  x.v96 = load16(short_tail, p.base + g.off + kStreamBase, p.zero + 16 * lane);
+}
+
 template <bool OFFS>
 DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
-                       const WaveLds& w) {
+                       const WaveLds& w, const GDesc& g, const GPre& x) {
   const uint32_t i = chunk * 64u + (uint32_t)lane;
   const bool valid = i < p.n;
-  const uint32_t ic = valid ? i : p.n - 1;  // clamped: descriptor loads without a branch
-  const uint32_t L = valid ? (uint32_t)p.len[ic] : 0u;
-  const uint64_t off = frame_off<OFFS>(p, ic);
-  uint32_t d[kPrefixDw];
-  load_prefix<0, 6>(p.base + off, L, reinterpret_cast<const uint8_t*>(p.tab), d);
-  // bytes 96..111 of frames shorter than 128 B, issued with the prefix: the
-  // end piece of their segment (no dependent load for those)
+  const uint32_t L = g.L;
+  const uint64_t off = g.off;
+  const uint32_t (&d)[kPrefixDw] = x.d;
+  const u32x4& v96 = x.v96;
   const bool short_tail = L > (uint32_t)kStreamBase && L < (uint32_t)kStreamBase + 32u;
-  u32x4 v96 = {0u, 0u, 0u, 0u};
-  if (__any(short_tail)) v96 = load16(short_tail, p.base + off + kStreamBase, p.zero + 16 * lane);
   LaneState s;
   const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
   if (__all(fixed))
     lane_parse<true, kPrefixDw>(p, T, d, L, s);
   else
-    lane_parse<false, kPrefixDw>(p, T, d, L, s);
+    lane_parse<false, kPrefixDw>(p, T, d, L, s, w.t6);
   // The 16-byte piece (counted from byte 96) holding the segment end is
   // summed by this lane, masked to the segment; streaming rounds read only
   // the whole pieces before it. A segment ending within 16 bytes past the
@@ -852,11 +880,37 @@ ixg_rx_fastc_s(KParams p) {
 // Every header shape the reference handles. Waves scan the defer flags 64
 // chunks at a time and process the flagged chunks (all chunks when
 // p.defer is null) one at a time.
+// Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
+// frame bytes one chunk ahead too, else loaded right before each chunk.
+template <bool OFFS, bool EARLY>
+DEV void gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
+                  uint32_t nq, int lane, GDesc D0) {
+  uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
+  GDesc D1;
+  gen_desc<OFFS>(p, c1, lane, D1);
+  GPre P0;
+  gen_pre(p, D0, lane, P0);
+  for (uint32_t j = 0; j < nq; j++) {
+    const uint32_t c2 = j + 2 < nq ? q[j + 2] : kNoChunk;
+    GDesc D2;
+    gen_desc<OFFS>(p, c2, lane, D2);
+    GPre P1;
+    if (EARLY) gen_pre(p, D1, lane, P1);
+    general_chunk<OFFS>(p, T, c0, lane, w, D0, P0);
+    if (!EARLY) gen_pre(p, D1, lane, P1);
+    c0 = c1;
+    c1 = c2;
+    D0 = D1;
+    D1 = D2;
+    P0 = P1;
+  }
+}
+
 template <bool OFFS>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
-      sh_sum[kWaves][64];
+      sh_sum[kWaves][64], sh_q[kWaves][64 * kQGroups];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
@@ -869,18 +923,41 @@ DEV void general_body(const KParams& p) {
     any = __ballot(ci < nchunks && p.defer[ci] != 0) != 0;
   }
   if (!__syncthreads_or(any)) return;
+  // IPv6 Toeplitz table (36 KiB, dynamic LDS: present only with IXG_F_IPV6)
+  extern __shared__ u32x4 dyn6[];
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < 36 * 256 / 4; k += kBlock) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
   stage_tables(p, T);
   const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
-                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave])};
-  for (uint32_t g = blockIdx.x * kWaves + wave; g < ngroups; g += nw) {
-    const uint32_t ci = g * 64u + (uint32_t)lane;
-    const bool want = ci < nchunks && (p.defer == nullptr || p.defer[ci] != 0);
-    uint64_t m = __ballot(want);
-    while (m) {
-      const uint32_t b = (uint32_t)__builtin_ctzll(m);
-      m &= m - 1;
-      general_chunk<OFFS>(p, T, g * 64u + b, lane, w);
+                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6)};
+  lds_u32* q = LDS(lds_u32, sh_q[wave]);
+  // groups g0, g0+nw, ... of this wave, kQGroups at a time: their deferred
+  // chunk ids go to an LDS list, which the pipeline then walks
+  for (uint32_t g0 = blockIdx.x * kWaves + wave; g0 < ngroups; g0 += kQGroups * nw) {
+    uint32_t nq = 0;
+#pragma unroll
+    for (int k = 0; k < kQGroups; k++) {
+      const uint32_t g = g0 + (uint32_t)k * nw;
+      const uint32_t ci = g * 64u + (uint32_t)lane;
+      const bool want = g < ngroups && ci < nchunks && (p.defer == nullptr || p.defer[ci] != 0);
+      const uint64_t m = __ballot(want);
+      if (want) q[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+      nq += (uint32_t)__popcll(m);
     }
+    __builtin_amdgcn_wave_barrier();
+    if (nq == 0) continue;
+    // Prefix prefetch one chunk ahead pays when chunks are parse-bound
+    // (short frames); when they stream, loading the next prefix during the
+    // rounds costs more than it hides. Decided once per list from its first
+    // chunk, as two separate loops, so no load in either is conditional.
+    GDesc D0;
+    gen_desc<OFFS>(p, q[0], lane, D0);
+    if (__any(D0.L > (uint32_t)kStreamBase + 32u))
+      gen_walk<OFFS, false>(p, T, w, q, nq, lane, D0);
+    else
+      gen_walk<OFFS, true>(p, T, w, q, nq, lane, D0);
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -907,16 +984,18 @@ static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
 static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
 static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
 
-static int occupancy(kern_fn k) {
-  // blocks per CU, cached per kernel (a handful of kernels, idempotent fill)
-  static kern_fn keys[16];
-  static int vals[16];
-  for (int i = 0; i < 16; i++) {
-    if (keys[i] == k) return vals[i];
+static int occupancy(kern_fn k, size_t shmem) {
+  // blocks per CU, cached per (kernel, dynamic LDS) (a handful; idempotent fill)
+  static kern_fn keys[32];
+  static size_t sizes[32];
+  static int vals[32];
+  for (int i = 0; i < 32; i++) {
+    if (keys[i] == k && sizes[i] == shmem) return vals[i];
     if (!keys[i]) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, shmem) != hipSuccess || nb < 1) nb = 1;
       vals[i] = nb;
+      sizes[i] = shmem;
       keys[i] = k;
       return nb;
     }
@@ -924,8 +1003,8 @@ static int occupancy(kern_fn k) {
   return 1;
 }
 
-static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu) {
-  const uint64_t cap = (uint64_t)ncu * (uint64_t)occupancy(k);
+static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 0) {
+  const uint64_t cap = (uint64_t)ncu * (uint64_t)occupancy(k, shmem);
   const uint64_t g = want < cap ? want : cap;
   return g ? (uint32_t)g : 1u;
 }
@@ -955,7 +1034,8 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, ncu)), dim3(kBlock), 0, (hipStream_t)stream, p);
   }
   const kern_fn kg = k_gen[gv][lay];
-  hipLaunchKernelGGL(kg, dim3(grid_for(kg, group_blocks, ncu)), dim3(kBlock), 0, (hipStream_t)stream, p);
+  const size_t sh6 = p.tab6 ? 36u * 256u * sizeof(uint32_t) : 0u;
+  hipLaunchKernelGGL(kg, dim3(grid_for(kg, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
 
