@@ -31,7 +31,13 @@ PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # one ixg_rx_batch_dev launch = the fixed-shape kernel + the general kernel
 # (which, when no chunk was deferred, only scans the per-chunk flags); the
 # HIP events bracket both on the launch stream
-KERNELS = {False: "ixg_rx_fast_s + ixg_rx_general_s", True: "ixg_rx_fast_o + ixg_rx_general_o"}
+def kernels(wl) -> str:
+    """The dispatches one launch makes (ixgrx_launch): the coalesced
+    fixed-shape kernel for fixed strides <= 64 B, else the lane-load one,
+    then the general kernel."""
+    if wl.off is not None:
+        return "ixg_rx_fast_o + ixg_rx_general_o"
+    return ("ixg_rx_fastc_s" if wl.stride <= 64 else "ixg_rx_fast_s") + " + ixg_rx_general_s"
 
 WORKLOADS = {
     # name: (trace kind, frames per GPU, distinct frames in the pool, description)
@@ -293,7 +299,7 @@ def main():
                      "frac": round(achieved / PEAK_HBM_GBPS, 4), "traffic": traffic,
                      "alg_bytes_per_pkt": round(wl.bytes_per_pkt, 2), "kernel_ms_avg": round(kavg * 1e3, 4),
                      "kernel_ms_min": round(kmin * 1e3, 4),
-                     "kernel": KERNELS[wl.off is not None],
+                     "kernel": kernels(wl),
                      "traffic_source": tsrc},
         "parity": "ok" if ok else "MISMATCH",
     }
