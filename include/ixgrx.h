@@ -198,6 +198,82 @@ struct ixg_rx_ops {
 uint32_t ixg_rx_dispatch(void *const *mbufs, const struct ixg_rx_rec *recs, uint32_t n,
 			 const struct ixg_rx_ops *ops, void *user);
 
+/* ---- PCB demux: the tcp_input step after the head ---- */
+
+/* For each IXG_V_TCP record, find the PCB the segment belongs to, exactly as
+ * tcp_input does (dp/net/tcp_in.c:233-323, 500-510): the active list of the
+ * frame's flow group at bucket tcp_to_idx (tcp_in.c:249,
+ * tcp_input_find_list :122-143), then the flow group's TIME-WAIT list
+ * (:260), then the per-CPU listen list (:273-304), else a RST. The tables
+ * are a snapshot of IX's lists, mirrored to the device by ixg_demux_load;
+ * entries keep list order, so "first match" is the reference's match. */
+
+/* One PCB as tcp_input_find_list compares it (tcp_in.c:134-138). */
+struct ixg_pcb_key {
+	uint32_t remote_ip;   /* pcb->remote_ip.addr: raw, network byte order */
+	uint32_t local_ip;    /* pcb->local_ip.addr */
+	uint16_t remote_port; /* pcb->remote_port: host order */
+	uint16_t local_port;  /* pcb->local_port */
+	uint32_t id;          /* the caller's handle for the PCB (returned as is) */
+};
+
+/* One LISTEN pcb as the listen walk compares it (tcp_in.c:274-303). */
+struct ixg_listen_key {
+	uint32_t local_ip;   /* lpcb->local_ip.addr; 0 = IP_ADDR_ANY */
+	uint16_t local_port; /* host order */
+	uint16_t rsvd;
+	uint32_t id;
+	uint32_t rsvd2;
+};
+
+/* A snapshot of one context's demux lists (host arrays; ixg_demux_load copies
+ * them). Flow groups are the context's local ones: fg_id - dev_idx*512. */
+struct ixg_demux_tables {
+	uint32_t nfg;                       /* flow groups in the snapshot (<= 512) */
+	uint32_t n_listen;
+	const uint32_t *active_start;       /* nfg*512 + 1 offsets: entries of
+	                                       fgs[g]->active_tbl[b].pcbs (ethfg.h:83) in
+	                                       list order are active[active_start[g*512+b] ..
+	                                       active_start[g*512+b+1]) */
+	const struct ixg_pcb_key *active;
+	const uint32_t *tw_start;           /* nfg + 1 offsets into tw[]: fgs[g]->tw_pcbs */
+	const struct ixg_pcb_key *tw;
+	const struct ixg_listen_key *listen; /* percpu tcp_cpu_lists.listen_pcbs, list order */
+};
+
+/* demux.kind */
+enum ixg_demux_kind {
+	IXG_D_NONE = 0,     /* not an IXG_V_TCP record */
+	IXG_D_ACTIVE = 1,   /* tcp_in.c:249-256: tcp_process on pcb `id` */
+	IXG_D_TIMEWAIT = 2, /* tcp_in.c:260-269: tcp_timewait_input on pcb `id` */
+	IXG_D_LISTEN = 3,   /* tcp_in.c:317-323: tcp_listen_input on lpcb `id`. As in the
+	                       reference's hlist walk, a non-empty listen list with no
+	                       port/address match yields its LAST entry (the loop
+	                       variable keeps the last node when no `break` ran) */
+	IXG_D_RESET = 4,    /* tcp_in.c:500-507: no PCB, tcp_rst sent */
+	IXG_D_DROP = 5,     /* tcp_in.c:503,509: no PCB, the segment carries RST: freed */
+};
+
+struct ixg_demux_rec {
+	uint32_t id;  /* the matched entry's id (0 for NONE/RESET/DROP) */
+	uint8_t kind; /* enum ixg_demux_kind */
+	uint8_t rsvd[3];
+};
+
+/* Load (replace) the context's demux tables. 0 or -errno. */
+int ixg_demux_load(void *ctx, const struct ixg_demux_tables *t);
+
+/* Device-resident: frames (as for ixg_rx_batch_dev) and the records that
+ * ixg_rx_batch_dev produced for them, in HBM; demux records into d_out.
+ * Asynchronous on `stream`. 0 or -errno (-ENOENT: no tables loaded). */
+int ixg_demux_batch_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec,
+			uint32_t n, struct ixg_demux_rec *d_out, void *stream);
+
+/* Host variant of ixg_demux_batch_dev (copies in, runs, copies out). */
+int ixg_demux_batch_host(void *ctx, const void *frames, const uint64_t *off, const uint16_t *len,
+			 uint32_t stride, uint32_t n, const struct ixg_rx_rec *rec,
+			 struct ixg_demux_rec *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,172 @@
+// ixgrx_demux.hip - MI355X (gfx950) PCB demux: the step of tcp_input that
+// follows the head (dp/net/tcp_in.c:233-323, 500-510), one lane per frame.
+//
+// Input: the frames and the 16-byte records ixg_rx_batch_dev produced for
+// them. For an IXG_V_TCP record the lane reads the 4-tuple from the frame
+// (IPv4 src/dst at bytes 26..33, ports at 14 + 4*ihl), then walks, in list
+// order, the active list of (flow group, pcb_bucket), the flow group's
+// TIME-WAIT list and the listen list, as tcp_input does. The lists are a CSR
+// mirror of IX's hlists (include/ixgrx.h struct ixg_demux_tables) in HBM;
+// they are small next to a batch and stay in L2 / Infinity Cache.
+//
+// A persistent grid-stride loop over 64-frame chunks; the record and the
+// frame's header bytes of the next chunk are loaded while the current chunk
+// walks its lists (dependent loads: that walk is the latency this hides).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ixgrx.h"
+#include "ixgrx_demux.h"
+
+#define DEV __device__ __forceinline__
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x2 u32x2_a4 __attribute__((aligned(4)));
+
+using DParams = ixg_dparams;
+
+DEV uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+
+// what a chunk's lane carries from the load stage to the walk stage
+struct Item {
+  u32x4 rec;   // the ixg_rx_rec as four dwords
+  u32x4 h0;    // frame bytes 12..27
+  u32x4 h1;    // frame bytes 28..43
+};
+
+template <bool OFFS>
+DEV uint64_t frame_off(const DParams& p, uint32_t i) {
+  return OFFS ? p.off[i] : (uint64_t)i * p.stride;
+}
+
+// loads are always issued (a valid dummy address when there is nothing to
+// read) so the compiler's vmcnt accounting stays exact across the pipeline
+template <bool OFFS>
+DEV void load_item(const DParams& p, uint32_t chunk, int lane, Item& it) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t ic = valid ? i : 0u;
+  it.rec = reinterpret_cast<const u32x4*>(p.rec)[ic];
+  const uint8_t* f = p.base + frame_off<OFFS>(p, ic);
+  it.h0 = *reinterpret_cast<const u32x4_a4*>(f + 12);
+  it.h1 = *reinterpret_cast<const u32x4_a4*>(f + 28);
+}
+
+// tcp_input_find_list (tcp_in.c:122-143): the first entry of [s, e) whose
+// (remote port, local port, remote ip, local ip) equals the segment's
+DEV bool find_list(const ixg_pcb_key* __restrict__ ent, uint32_t s, uint32_t e, uint32_t sport, uint32_t dport,
+                   uint32_t src, uint32_t dst, uint32_t& id) {
+  const uint32_t ports = sport | (dport << 16);
+  for (uint32_t k = s; k < e; k++) {
+    const u32x4 v = reinterpret_cast<const u32x4*>(ent)[k];
+    if (v.z == ports && v.x == src && v.y == dst) {
+      id = v.w;
+      return true;
+    }
+  }
+  return false;
+}
+
+template <bool OFFS>
+DEV void walk_item(const DParams& p, uint32_t i, const Item& it) {
+  const uint32_t verdict = (it.rec.x >> 16) & 0xffu;
+  uint32_t kind = IXG_D_NONE, id = 0;
+  if (verdict == IXG_V_TCP) {
+    const uint32_t fg = (it.rec.x & 0xffffu) - p.fg_base;  // ethfg: fgs[pkt->fg_id]
+    const uint32_t bucket = it.rec.w & 0xffffu;             // tcp_to_idx (tcp_in.c:233)
+    const uint32_t tflags = (it.rec.w >> 16) & 0xffu;
+    const uint32_t ihl = (it.h0.x >> 16) & 15u;             // frame byte 14
+    // src = bytes 26..29, dst = bytes 30..33 (raw, network order as loaded LE)
+    const uint32_t src = (it.h0.w >> 16) | (it.h1.x << 16);
+    const uint32_t dst = (it.h1.x >> 16) | (it.h1.y << 16);
+    uint32_t sw, dw;  // ports: L4 bytes 0..3 at 14 + 4*ihl
+    if (ihl == 5) {
+      sw = it.h1.y >> 16;
+      dw = it.h1.z & 0xffffu;
+    } else {  // IP options: one more (dependent) load, rare
+      const uint8_t* f = p.base + frame_off<OFFS>(p, i);
+      const u32x2 v = *reinterpret_cast<const u32x2_a4*>(f + 12 + 4 * ihl);
+      sw = v.x >> 16;
+      dw = v.y & 0xffffu;
+    }
+    const uint32_t sport = bswap16(sw), dport = bswap16(dw);  // tcp_in.c:230-231
+    bool hit = false;
+    if (fg < p.nfg) {
+      const uint32_t a = fg * IXG_PCB_BUCKETS + bucket;
+      hit = find_list(p.active, p.active_start[a], p.active_start[a + 1], sport, dport, src, dst, id);
+      if (hit) {
+        kind = IXG_D_ACTIVE;  // tcp_in.c:249-256
+      } else if (find_list(p.tw, p.tw_start[fg], p.tw_start[fg + 1], sport, dport, src, dst, id)) {
+        kind = IXG_D_TIMEWAIT;  // tcp_in.c:260-269
+        hit = true;
+      }
+    }
+    if (!hit) {
+      // tcp_in.c:273-304 without SO_REUSE / LWIP_IPV6 (opt.h:1579,2016):
+      // break at the first lpcb on the port whose address is the segment's
+      // destination or ANY; the hlist loop variable keeps the last entry
+      // when nothing breaks, so a non-empty list always yields an lpcb
+      if (p.n_listen != 0) {
+        uint32_t k = 0;
+        for (; k < p.n_listen; k++) {
+          const u32x4 v = reinterpret_cast<const u32x4*>(p.listen)[k];
+          if ((v.y & 0xffffu) == dport && (v.x == dst || v.x == 0u)) break;
+        }
+        if (k == p.n_listen) k = p.n_listen - 1;
+        id = reinterpret_cast<const u32x4*>(p.listen)[k].z;
+        kind = IXG_D_LISTEN;  // tcp_in.c:317-323
+      } else {
+        kind = (tflags & 0x04u) ? IXG_D_DROP : IXG_D_RESET;  // tcp_in.c:500-510 (TCP_RST = 0x04)
+        id = 0;
+      }
+    }
+  }
+  const u32x2 o = {id, kind};
+  reinterpret_cast<u32x2*>(p.out)[i] = o;
+}
+
+template <bool OFFS>
+DEV void demux_loop(const DParams& p) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * kWaves;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  Item cur;
+  load_item<OFFS>(p, c, lane, cur);
+  for (;;) {
+    const uint32_t cn = c + nw;
+    Item nxt;
+    load_item<OFFS>(p, cn < nchunks ? cn : c, lane, nxt);
+    const uint32_t i = c * 64u + (uint32_t)lane;
+    if (i < p.n) walk_item<OFFS>(p, i, cur);
+    c = cn;
+    if (c >= nchunks) break;
+    cur = nxt;
+  }
+}
+
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_demux_s(DParams p) { demux_loop<false>(p); }
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_demux_o(DParams p) { demux_loop<true>(p); }
+
+extern "C" int ixgrx_demux_launch(const void* params, uint32_t ncu, void* stream) {
+  const DParams& p = *static_cast<const DParams*>(params);
+  const uint64_t nchunks = ((uint64_t)p.n + 63u) / 64u;
+  const uint64_t want = (nchunks + kWaves - 1) / kWaves;
+  void (*k)(DParams) = p.off ? ixg_demux_o : ixg_demux_s;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+  const uint64_t cap = (uint64_t)ncu * (uint64_t)nb;
+  const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+  hipLaunchKernelGGL(k, dim3(grid ? grid : 1u), dim3(kBlock), 0, (hipStream_t)stream, p);
+  return (int)hipGetLastError();
+}

@@ -14,6 +14,7 @@
 
 #include "../../include/ixgrx.h"
 #include "ixgrx_internal.h"
+#include "ixgrx_demux.h"
 
 struct ixg_ctx {
 	int device;
@@ -41,6 +42,14 @@ struct ixg_ctx {
 	struct ixg_rx_rec *d_out;
 	uint32_t *d_csum;
 	size_t d_n_cap;
+	/* PCB demux tables (ixg_demux_load) */
+	int demux_loaded;
+	uint32_t dmx_nfg, dmx_nlisten;
+	uint32_t *d_astart, *d_twstart;
+	struct ixg_pcb_key *d_active, *d_tw;
+	struct ixg_listen_key *d_listen;
+	struct ixg_demux_rec *d_dmx; /* host-path output staging */
+	size_t d_dmx_cap;
 };
 
 /* ---- hash tables -------------------------------------------------------- */
@@ -121,6 +130,7 @@ const char *ixg_strerror(int err)
 	case -ENOMEM: return "out of memory";
 	case -ENODEV: return "no such HIP device";
 	case -EIO: return "HIP runtime error";
+	case -ENOENT: return "no demux tables loaded";
 	default: return "unknown error";
 	}
 }
@@ -148,6 +158,12 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_len);
 	hipFree(c->d_out);
 	hipFree(c->d_csum);
+	hipFree(c->d_astart);
+	hipFree(c->d_twstart);
+	hipFree(c->d_active);
+	hipFree(c->d_tw);
+	hipFree(c->d_listen);
+	hipFree(c->d_dmx);
 	hipHostFree(c->h_frames);
 	hipHostFree(c->h_off);
 	hipHostFree(c->h_len);
@@ -453,4 +469,137 @@ uint32_t ixg_rx_dispatch(void *const *mbufs, const struct ixg_rx_rec *recs, uint
 			fn(user, mbufs ? mbufs[i] : NULL, r);
 	}
 	return delivered;
+}
+
+/* ---- PCB demux (tcp_in.c:233-323, 500-510) --------------------------------- */
+
+static int upload(void **dst, const void *src, size_t bytes)
+{
+	hipFree(*dst);
+	*dst = NULL;
+	if (!bytes)
+		return 0;
+	HIPCHK(hipMalloc(dst, bytes));
+	HIPCHK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+	return 0;
+}
+
+static int csr_ok(const uint32_t *start, size_t rows)
+{
+	if (!start || start[0] != 0)
+		return 0;
+	for (size_t r = 0; r < rows; r++)
+		if (start[r + 1] < start[r])
+			return 0;
+	return 1;
+}
+
+int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !t || t->nfg > IXG_ETH_MAX_NUM_FG)
+		return -EINVAL;
+	const size_t na_rows = (size_t)t->nfg * IXG_PCB_BUCKETS;
+	if (!csr_ok(t->active_start, na_rows) || !csr_ok(t->tw_start, t->nfg))
+		return -EINVAL;
+	const size_t na = t->active_start[na_rows], ntw = t->tw_start[t->nfg];
+	if ((na && !t->active) || (ntw && !t->tw) || (t->n_listen && !t->listen))
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	c->demux_loaded = 0;
+	int rc;
+	if ((rc = upload((void **)&c->d_astart, t->active_start, (na_rows + 1) * sizeof(uint32_t))) ||
+	    (rc = upload((void **)&c->d_twstart, t->tw_start, ((size_t)t->nfg + 1) * sizeof(uint32_t))) ||
+	    (rc = upload((void **)&c->d_active, t->active, na * sizeof(struct ixg_pcb_key))) ||
+	    (rc = upload((void **)&c->d_tw, t->tw, ntw * sizeof(struct ixg_pcb_key))) ||
+	    (rc = upload((void **)&c->d_listen, t->listen, (size_t)t->n_listen * sizeof(struct ixg_listen_key))))
+		return rc;
+	c->dmx_nfg = t->nfg;
+	c->dmx_nlisten = t->n_listen;
+	c->demux_loaded = 1;
+	return 0;
+}
+
+static int demux_launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, uint32_t stride, uint32_t n,
+			const struct ixg_rx_rec *rec, struct ixg_demux_rec *out, hipStream_t s)
+{
+	struct ixg_dparams p;
+	memset(&p, 0, sizeof(p));
+	p.base = base;
+	p.off = off;
+	p.rec = rec;
+	p.out = out;
+	p.active_start = c->d_astart;
+	p.active = c->d_active;
+	p.tw_start = c->d_twstart;
+	p.tw = c->d_tw;
+	p.listen = c->d_listen;
+	p.stride = stride;
+	p.n = n;
+	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
+	p.nfg = c->dmx_nfg;
+	p.n_listen = c->dmx_nlisten;
+	return ixgrx_demux_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
+}
+
+int ixg_demux_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec, uint32_t n,
+			struct ixg_demux_rec *d_out, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || (n && (!fr->base || !d_rec || !d_out)))
+		return -EINVAL;
+	if (!c->demux_loaded)
+		return -ENOENT;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)fr->base & 3) || (!fr->off && (fr->stride & 3)) || ((uintptr_t)d_rec & 15) ||
+	    ((uintptr_t)d_out & 7) || ((uintptr_t)fr->off & 7))
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	return demux_launch(c, (const uint8_t *)fr->base, fr->off, fr->stride, n, d_rec, d_out, (hipStream_t)stream);
+}
+
+int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, const uint16_t *len, uint32_t stride,
+			 uint32_t n, const struct ixg_rx_rec *rec, struct ixg_demux_rec *out)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && (!frames || !len || !rec || !out)))
+		return -EINVAL;
+	if (!c->demux_loaded)
+		return -ENOENT;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)frames & 3) || (!off && (stride & 3)))
+		return -EINVAL;
+	uint64_t end = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		uint64_t o = off ? off[i] : (uint64_t)i * stride;
+		if (o & 3)
+			return -EINVAL;
+		if (o + len[i] > end)
+			end = o + len[i];
+	}
+	HIPCHK(hipSetDevice(c->device));
+	int rc = grow_dev(c, (size_t)end + IXG_TAIL_PAD, n);
+	if (rc)
+		return rc;
+	if (n > c->d_dmx_cap) {
+		hipFree(c->d_dmx);
+		c->d_dmx = NULL;
+		c->d_dmx_cap = 0;
+		HIPCHK(hipMalloc((void **)&c->d_dmx, (size_t)c->d_n_cap * sizeof(struct ixg_demux_rec)));
+		c->d_dmx_cap = c->d_n_cap;
+	}
+	HIPCHK(hipMemcpyAsync(c->d_frames, frames, (size_t)end, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemsetAsync(c->d_frames + end, 0, IXG_TAIL_PAD, c->stream));
+	if (off)
+		HIPCHK(hipMemcpyAsync(c->d_off, off, n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->d_out, rec, n * sizeof(*rec), hipMemcpyHostToDevice, c->stream));
+	rc = demux_launch(c, c->d_frames, off ? c->d_off : NULL, stride, n, c->d_out, c->d_dmx, c->stream);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(out, c->d_dmx, n * sizeof(*out), hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
 }

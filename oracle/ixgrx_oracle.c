@@ -4,7 +4,7 @@
  * TEST INFRASTRUCTURE ONLY (see ixgrx_oracle.h). Every function cites the
  * reference file:line it restates (paths relative to /root/reference).
  * Pinned against golden vectors from the reference's own code
- * (tests/golden/*.npz, made by tests/golden/make_golden.py through
+ * (the .npz files under tests/golden/, made by tests/golden/make_golden.py through
  * oracle/ref_harness) and against the public RSS verification vectors.
  *
  * Semantics that live in NIC silicon rather than in the tree (IX offloads
@@ -615,4 +615,86 @@ int ixgo_rx_batch_mbufs(const struct ixg_rx_cfg *cfg, void *const *mbufs, uint32
 {
 	struct job j = {cfg, NULL, NULL, NULL, NULL, mbufs, 0, 0, 0, out, NULL, work};
 	return run_batch(&j, n, threads, hash_mode);
+}
+
+/* ---- PCB demux: tcp_input after the head ---------------- */
+
+/* tcp_input_find_list (dp/net/tcp_in.c:122-143) over the list
+ * ent[s..e) in list order: remote_port == tcphdr->src, local_port ==
+ * tcphdr->dest (host order after tcp_in.c:230-231), remote_ip == current
+ * source, local_ip == current destination (IP_PCB_IPVER_INPUT_MATCH is 1
+ * without LWIP_IPV6, lwip/ip.h:99). */
+static const struct ixg_pcb_key *find_list(const struct ixg_pcb_key *ent, uint32_t s, uint32_t e,
+					   uint16_t src_port, uint16_t dst_port, uint32_t src_raw,
+					   uint32_t dst_raw)
+{
+	for (uint32_t k = s; k < e; k++) {
+		const struct ixg_pcb_key *pcb = &ent[k];
+		if (pcb->remote_port == src_port && pcb->local_port == dst_port &&
+		    pcb->remote_ip == src_raw && pcb->local_ip == dst_raw)
+			return pcb;
+	}
+	return NULL;
+}
+
+void ixgo_demux_one(const struct ixg_demux_tables *t, uint32_t fg_base, const uint8_t *frame, uint32_t len,
+		    const struct ixg_rx_rec *rec, struct ixg_demux_rec *out)
+{
+	memset(out, 0, sizeof(*out));
+	out->kind = IXG_D_NONE;
+	if (rec->verdict != IXG_V_TCP) /* only tcp_input_tmp's segments reach tcp_input (ip.c:93-96) */
+		return;
+	struct frame f = {frame, len};
+	uint32_t ihl = B(&f, 14) & 15u, l4 = 14 + 4 * ihl;
+	uint32_t src = Braw32(&f, 26), dst = Braw32(&f, 30);
+	uint16_t sport = B16(&f, l4), dport = B16(&f, l4 + 2); /* ntohs, tcp_in.c:230-231 */
+	uint32_t fg = (uint32_t)rec->fg_id - fg_base;            /* cur_fg = fgs[pkt->fg_id], ip.c:125 */
+	if (fg < t->nfg) {
+		/* active_tbl[idx] with idx = tcp_to_idx (tcp_in.c:233,249) */
+		uint32_t a = fg * IXG_PCB_BUCKETS + rec->pcb_bucket;
+		const struct ixg_pcb_key *pcb =
+			find_list(t->active, t->active_start[a], t->active_start[a + 1], sport, dport, src, dst);
+		if (pcb) {
+			out->kind = IXG_D_ACTIVE; /* tcp_in.c:250-256 */
+			out->id = pcb->id;
+			return;
+		}
+		pcb = find_list(t->tw, t->tw_start[fg], t->tw_start[fg + 1], sport, dport, src, dst);
+		if (pcb) {
+			out->kind = IXG_D_TIMEWAIT; /* tcp_in.c:260-269 */
+			out->id = pcb->id;
+			return;
+		}
+	}
+	/* tcp_in.c:273-304, SO_REUSE 0 (opt.h:1579), LWIP_IPV6 0 (opt.h:2016):
+	 * hlist_for_each (inc/ix/list.h:731-732) assigns lpcb on every
+	 * iteration, so a walk that never breaks leaves lpcb = the last entry */
+	const struct ixg_listen_key *lpcb = NULL;
+	for (uint32_t k = 0; k < t->n_listen; k++) {
+		lpcb = &t->listen[k];
+		if (lpcb->local_port == dport) {
+			if (lpcb->local_ip == dst)
+				break; /* exact match (:290-292) */
+			else if (lpcb->local_ip == 0)
+				break; /* ANY match (:293-300) */
+		}
+	}
+	if (lpcb) {
+		out->kind = IXG_D_LISTEN; /* tcp_in.c:317-323 */
+		out->id = lpcb->id;
+		return;
+	}
+	/* no PCB: tcp_rst unless the segment is itself a RST (tcp_in.c:500-510) */
+	out->kind = (rec->tcp_flags & 0x04) ? IXG_D_DROP : IXG_D_RESET;
+}
+
+int ixgo_demux_batch(const struct ixg_demux_tables *t, uint32_t fg_base, const uint8_t *base, const uint64_t *off,
+		     const uint16_t *len, uint32_t stride, uint32_t n, const struct ixg_rx_rec *rec,
+		     struct ixg_demux_rec *out)
+{
+	for (uint32_t i = 0; i < n; i++) {
+		uint64_t o = off ? off[i] : (uint64_t)i * stride;
+		ixgo_demux_one(t, fg_base, base + o, len[i], &rec[i], &out[i]);
+	}
+	return 0;
 }

@@ -129,3 +129,35 @@ def ref_time(tr, key: bytes, seconds: float, nb: int = 128, dev: int = 0, flags:
     d = json.loads(r.stdout.strip().splitlines()[-1])
     return 1e9 / d["ns_per_pkt"], f"oracle/_ref/ixref_rx (reference dp/net + dp/lwip objects) over {n} frames x " \
                                   f"{d['pkts'] // n} passes in {d['seconds']:.1f}s, 1 core"
+
+
+class _DemuxTables(ctypes.Structure):
+    _fields_ = [("nfg", ctypes.c_uint32), ("n_listen", ctypes.c_uint32), ("active_start", ctypes.c_void_p),
+                ("active", ctypes.c_void_p), ("tw_start", ctypes.c_void_p), ("tw", ctypes.c_void_p),
+                ("listen", ctypes.c_void_p)]
+
+
+def demux_batch(nfg: int, active_start, active, tw_start, tw, listen, fg_base: int, blob: np.ndarray, off,
+                lens: np.ndarray, stride: int, rec: np.ndarray) -> np.ndarray:
+    """ixgo_demux_batch (tcp_in.c:233-323, 500-510) over the CSR lists;
+    returns the 8-byte demux records as an (n, 8) u8 array."""
+    L = lib()
+    if not hasattr(L, "_demux_bound"):
+        vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+        L.ixgo_demux_batch.argtypes = [ctypes.POINTER(_DemuxTables), u32, vp, vp, vp, u32, u32, vp, vp]
+        L.ixgo_demux_batch.restype = i32
+        L._demux_bound = True
+    arrs = [np.ascontiguousarray(a) for a in (active_start, active, tw_start, tw, listen)]
+    t = _DemuxTables()
+    t.nfg = nfg
+    t.n_listen = len(arrs[4])
+    t.active_start, t.active, t.tw_start, t.tw, t.listen = [a.ctypes.data if a.size else None for a in arrs]
+    n = int(lens.shape[0])
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    lens = np.ascontiguousarray(lens, dtype=np.uint16)
+    offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    rec = np.ascontiguousarray(rec).view(np.uint8).reshape(n, 16)
+    out = np.zeros((n, 8), dtype=np.uint8)
+    L.ixgo_demux_batch(ctypes.byref(t), fg_base, blob.ctypes.data, None if offa is None else offa.ctypes.data,
+                       lens.ctypes.data, stride, n, rec.ctypes.data, out.ctypes.data)
+    return out

@@ -26,4 +26,12 @@ int ref_pbuf_header_rom(uint16_t len, int16_t inc, uint16_t *new_len);
 int ref_tcp_to_idx(uint32_t local_raw, uint32_t remote_raw, uint16_t local_port, uint16_t remote_port);
 uint32_t ref_toeplitz(const uint8_t *key, uint32_t src_raw, uint32_t dst_raw, uint16_t sport_raw,
 		      uint16_t dport_raw);
+
+/* a PCB as the demux harness hands it to ref_find_list (ref_tcpin.c) */
+struct ref_pcb {
+	uint32_t remote_ip, local_ip; /* raw, network order */
+	uint16_t remote_port, local_port; /* host order */
+};
+int ref_find_list(const struct ref_pcb *pcbs, int n, uint32_t src_raw, uint32_t dst_raw, uint16_t src_port,
+		  uint16_t dst_port);
 #endif

@@ -16,8 +16,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 
 
-def golden_names():
-    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+def golden_names(prefix: str = ""):
+    """RX fixtures by default; demux fixtures are the ones named demux_*."""
+    names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+    if prefix:
+        return [n for n in names if n.startswith(prefix)]
+    return [n for n in names if not n.startswith("demux")]
 
 
 def load_golden(name):
@@ -27,6 +31,13 @@ def load_golden(name):
 
 @pytest.fixture(params=golden_names())
 def golden(request):
+    g = load_golden(request.param)
+    g["name"] = request.param
+    return g
+
+
+@pytest.fixture(params=golden_names("demux"))
+def golden_demux(request):
     g = load_golden(request.param)
     g["name"] = request.param
     return g
