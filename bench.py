@@ -66,13 +66,13 @@ def alg_bytes(tr) -> np.ndarray:
 class Workload:
     """A batch of n frames on `dev`, tiled from `pool` distinct frames."""
 
-    def __init__(self, name: str, seed: int, dev, n: int | None = None):
+    def __init__(self, name: str, seed: int, dev, n: int | None = None, pool: int | None = None):
         import torch
         from ix_amd import traces
-        kind, n_def, pool, self.desc = WORKLOADS[name]
+        kind, n_def, pool_def, self.desc = WORKLOADS[name]
         self.name = name
         self.n = n or n_def
-        pool = min(pool, self.n)
+        pool = min(pool or pool_def, self.n)
         assert self.n % pool == 0
         self.reps = self.n // pool
         self.pool = traces.make_trace(kind, pool, seed=seed)
@@ -104,13 +104,14 @@ class Workload:
         eng.batch_dev(self.blob.data_ptr(), None if self.off is None else self.off.data_ptr(),
                       self.len.data_ptr(), self.stride, self.n, self.out.data_ptr(), None, stream)
 
-    def check(self, key: bytes) -> bool:
-        """Records of the tiled batch == the oracle's records of the pool, tiled."""
+    def snapshot(self):
+        """Device-side tiling check (every repetition of the pool produced
+        the same records as the first) and the first repetition's records,
+        for the cpu_baseline leg to compare with the oracle."""
         import torch
-        from oracle import oracle
-        er, _ = oracle.rx_trace(self.pool, key, flags=self.flags, threads=8, hash_mode=oracle.HASH_TABLE)
-        exp = torch.from_numpy(er).to(self.out.device)
-        return bool(torch.equal(self.out.view(self.reps, -1, 16), exp.unsqueeze(0).expand(self.reps, -1, -1)))
+        v = self.out.view(self.reps, -1, 16)
+        tiled = bool(torch.equal(v, v[:1].expand(self.reps, -1, -1)))
+        return tiled, v[0].cpu().numpy()
 
 
 def time_steps(wl, eng, steps, warmup, dist, world):
@@ -197,6 +198,30 @@ def cpu_baseline(tr, flags, key, seconds: float, threads: int, name: str):
             "reference_sample": rdesc}
 
 
+def parity_leg(checks, key) -> dict:
+    """The oracle checks the device results of every line (part of the
+    cpu_baseline leg: the oracle is only ever the checker). A line passes
+    when its tiled batch is self-consistent on the device and its first
+    repetition equals the oracle's records for the distinct frames."""
+    from ix_amd import demux
+    from oracle import oracle
+    res = {}
+    for c in checks:
+        if c[0] == "rx":
+            _, name, pool, flags, rec, tiled = c
+            er, _ = oracle.rx_trace(pool, key, flags=flags, threads=8, hash_mode=oracle.HASH_TABLE)
+            res[name] = "ok" if tiled and np.array_equal(rec, er) else "MISMATCH"
+        else:
+            _, pool, tabs, rec, dmx, tiled = c
+            er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
+            exp = oracle.demux_batch(tabs.nfg, tabs.active_start, tabs.active, tabs.tw_start, tabs.tw, tabs.listen,
+                                     0, pool.blob, pool.off, pool.len, pool.stride, er)
+            ok = tiled and np.array_equal(rec, er) and np.array_equal(dmx, exp)
+            res["demux"] = "ok" if ok else "MISMATCH"
+            res["demux_kinds"] = {demux.KINDS[int(v)]: int(n) for v, n in zip(*np.unique(exp[:, 4], return_counts=True))}
+    return res
+
+
 def copy_inclusive(wl, eng, key, reps=3):
     """Host-resident batch: H2D frames (pinned) + kernel + D2H records."""
     import torch
@@ -224,6 +249,61 @@ def copy_inclusive(wl, eng, key, reps=3):
             "link_gbps": (h2d + n * 16) / best / 1e9}
 
 
+def demux_line(dev, key, steps: int, rank: int, eng_for):
+    """PCB demux over C2's shape: 16M 64-B TCP frames tiled
+    from 2^16 distinct connections, every one ESTABLISHED (the echoserver
+    case), 1% extra TIME-WAIT entries and one listener. The RX records are
+    made on the GPU first; a step = one ixg_demux_batch_dev launch."""
+    import torch
+    from ix_amd import demux
+    wl = Workload("c2", seed=0x1BD000 + 97 * rank, dev=dev, pool=1 << 16)
+    eng = eng_for(0)
+    stream = torch.cuda.current_stream()
+    wl.launch(eng, stream.cuda_stream)
+    pool = wl.pool
+    keys = demux.tcp_keys(pool.blob, pool.offsets())
+    cfg = eng.cfg
+    rng = np.random.default_rng(1)
+    tw = keys[rng.random(keys.size) < 0.01].copy()
+    tw["id"] += 1 << 20
+    tw["remote_port"] ^= 1  # TIME-WAIT entries of other (closed) connections
+    lis = np.array([(0, 80, 0, 7, 0)], dtype=demux.LISTEN_DTYPE)
+    tabs = demux.DemuxTables.build(cfg, keys, tw, lis)
+    demux.load(eng, tabs)
+    out = torch.empty((wl.n, 8), dtype=torch.uint8, device=dev)
+
+    def launch():
+        demux.batch_dev(eng, wl.blob.data_ptr(), None, wl.stride, wl.n, wl.out.data_ptr(), out.data_ptr(),
+                        stream.cuda_stream)
+    for _ in range(3):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        launch()
+        b.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = float(np.mean([a.elapsed_time(b) * 1e-3 for a, b in ev]))
+    v = out.view(wl.reps, -1, 8)
+    tiled = bool(torch.equal(v, v[:1].expand(wl.reps, -1, -1)))
+    check = ("demux", pool, tabs, wl.out.view(wl.reps, -1, 16)[0].cpu().numpy(), v[0].cpu().numpy(), tiled)
+    # algorithmic bytes per frame: the record (16), the header bytes the
+    # lookup reads (byte 14 + the 12 tuple bytes), the bucket bounds (8), the
+    # entries compared up to the match (16 each, here ~1 per bucket) and
+    # the 8-byte result
+    cmp = 1.0
+    alg = 16 + 13 + 8 + 16 * cmp + 8
+    return {"workload": "PCB demux over C2: 16M x 64B TCP frames, 65536 established connections, 1% TIME-WAIT, "
+                        "1 listener (kernel ixg_demux_s)",
+            "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
+            "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4),
+            "frame_bytes_touched_per_pkt": 60 + 16 + 8,
+            "parity": "pending"}, check
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -246,6 +326,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy", action="store_true")
+    ap.add_argument("--no-demux", action="store_true")
     ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
     args = ap.parse_args()
 
@@ -271,8 +352,10 @@ def main():
 
     wl = Workload(args.workload, seed=0x1B0000 + 2 + 97 * rank, dev=dev, n=args.n)
     el, kavg, kmin = time_steps(wl, engine(wl.flags), args.steps, args.warmup, dist, world)
-    ok = wl.check(key) if rank == 0 else True
+    tiled, first = wl.snapshot()
+    checks = [("rx", wl.name, wl.pool, wl.flags, first, tiled)]
     primary = (wl.name, wl.pool, wl.flags)
+    wl_name = wl.name
     total = wl.n * args.steps * world
     mpps = total / el / 1e6
     bpl = wl.bytes_per_pkt * wl.n  # algorithmic bytes per launch (one GPU)
@@ -301,22 +384,29 @@ def main():
                      "kernel_ms_min": round(kmin * 1e3, 4),
                      "kernel": kernels(wl),
                      "traffic_source": tsrc},
-        "parity": "ok" if ok else "MISMATCH",
+        "parity": "tiled-consistent" if tiled else "MISMATCH",
     }
     if args.secondary and args.secondary != args.workload:
         del wl
         torch.cuda.empty_cache()
         wl2 = Workload(args.secondary, seed=0x1B0000 + 4 + 97 * rank, dev=dev)
         el2, k2, _ = time_steps(wl2, engine(wl2.flags), max(5, args.steps // 2), 2, dist, world)
-        ok2 = wl2.check(key) if rank == 0 else True
+        tiled2, first2 = wl2.snapshot()
+        checks.append(("rx", wl2.name, wl2.pool, wl2.flags, first2, tiled2))
         m2 = wl2.n * max(5, args.steps // 2) * world / el2 / 1e6
         a2 = wl2.bytes_per_pkt * wl2.n / k2 / 1e9
         res["secondary"] = {"workload": wl2.desc, "mpps": round(m2, 2),
                             "gbps_algorithmic": round(m2 * wl2.bytes_per_pkt / 1e3, 1),
                             "roofline_frac": round(a2 / PEAK_HBM_GBPS, 4), "kernel_ms_avg": round(k2 * 1e3, 4),
                             "alg_bytes_per_pkt": round(wl2.bytes_per_pkt, 1),
-                            "parity": "ok" if ok2 else "MISMATCH"}
+                            "parity": "tiled-consistent" if tiled2 else "MISMATCH"}
         wl = wl2
+    if not args.no_demux and args.workload == "c2":
+        del wl
+        torch.cuda.empty_cache()
+        res["demux"], dchk = demux_line(dev, key, max(5, args.steps // 2), rank, engine)
+        checks.append(dchk)
+        wl = None
     if rank == 0 and world == 1 and not args.no_copy:
         del wl
         torch.cuda.empty_cache()
@@ -327,6 +417,14 @@ def main():
         threads = min(16, os.cpu_count() or 1)
         pname, ptr, pflags = primary
         res["cpu_baseline"] = cpu_baseline(ptr, pflags, key, args.cpu_seconds, threads, pname)
+        par = parity_leg(checks, key)
+        res["cpu_baseline"]["parity_vs_oracle"] = par
+        res["parity"] = par[wl_name]
+        if "secondary" in res:
+            res["secondary"]["parity"] = par[args.secondary]
+        if "demux" in res:
+            res["demux"]["parity"] = par["demux"]
+            res["demux"]["kinds"] = par["demux_kinds"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -160,3 +160,23 @@ def batch_host(eng: ixgrx.RxEngine, blob: np.ndarray, off, lens: np.ndarray, str
                                           lens.ctypes.data, stride, n, rec.ctypes.data, out.ctypes.data),
                  "ixg_demux_batch_host", lib)
     return out
+
+
+def tcp_keys(blob: np.ndarray, offsets: np.ndarray) -> np.ndarray:
+    """PCB keys (remote = source, local = destination) of IPv4 frames at
+    `offsets`, read as the demux kernel reads them: IP src/dst at bytes
+    26..33, ports at 14 + 4*ihl. For building synthetic connection tables."""
+    o = np.asarray(offsets, dtype=np.int64)
+    b = blob
+
+    def le32(p):
+        return (b[p].astype(np.uint32) | (b[p + 1].astype(np.uint32) << 8) | (b[p + 2].astype(np.uint32) << 16)
+                | (b[p + 3].astype(np.uint32) << 24))
+    l4 = o + 14 + 4 * (b[o + 14] & 15).astype(np.int64)
+    k = np.zeros(o.size, PCB_DTYPE)
+    k["remote_ip"] = le32(o + 26)
+    k["local_ip"] = le32(o + 30)
+    k["remote_port"] = (b[l4].astype(np.uint32) << 8) | b[l4 + 1]
+    k["local_port"] = (b[l4 + 2].astype(np.uint32) << 8) | b[l4 + 3]
+    k["id"] = np.arange(o.size, dtype=np.uint32)
+    return k
