@@ -25,6 +25,8 @@ struct ixg_ctx {
 	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
 	uint8_t *d_defer;    /* one flag per 64-packet chunk */
 	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
+	uint32_t *d_present; /* [3] per-class stamps (ixg_kparams.present) */
+	uint32_t epoch;      /* last launch's stamp */
 	size_t defer_cap;
 	uint64_t *d_tab;
 	uint32_t *d_tab6;
@@ -153,6 +155,7 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_tab6);
 	hipFree(c->d_defer);
 	hipFree(c->d_zero);
+	hipFree(c->d_present);
 	hipFree(c->d_frames);
 	hipFree(c->d_off);
 	hipFree(c->d_len);
@@ -205,6 +208,8 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		c->fast_variant = e ? (atoi(e) & 0xff) : 0;
 		e = getenv("IXGRX_GEN_VARIANT");
 		c->fast_variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
+		e = getenv("IXGRX_SHORT_VARIANT");
+		c->fast_variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
 	}
 	c->ncu = (uint32_t)prop.multiProcessorCount;
 	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
@@ -234,7 +239,9 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		free(t6);
 	}
 	if (hipMalloc((void **)&c->d_zero, IXG_ZERO_PAGE) != hipSuccess ||
-	    hipMemset(c->d_zero, 0, IXG_ZERO_PAGE) != hipSuccess)
+	    hipMemset(c->d_zero, 0, IXG_ZERO_PAGE) != hipSuccess ||
+	    hipMalloc((void **)&c->d_present, 4 * sizeof(uint32_t)) != hipSuccess ||
+	    hipMemset(c->d_present, 0, 4 * sizeof(uint32_t)) != hipSuccess)
 		goto fail;
 	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
@@ -278,6 +285,10 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 			c->defer_cap = cap;
 		}
 		p.defer = c->d_defer;
+		p.present = c->d_present;
+		if (++c->epoch == 0)
+			c->epoch = 1;
+		p.epoch = c->epoch;
 	}
 	return ixgrx_launch(&p, c->fast_variant, c->ncu, s) == 0 ? 0 : -EIO;
 }

@@ -26,14 +26,26 @@ struct ixg_kparams {
 	uint32_t flags;
 	uint32_t fg_base;      /* dev_idx * 512 */
 	uint32_t fg_mask;      /* nb_rx_fgs - 1 */
-	uint8_t *defer;        /* per 64-packet chunk: 1 = left for the general
-	                          kernel; NULL = general kernel does everything */
+	uint8_t *defer;        /* per 64-packet chunk: 0 = done by the fixed-shape
+	                          kernel, IXG_CLS_SHORT / IXG_CLS_LONG = left for
+	                          that general kernel; NULL = the long general
+	                          kernel does everything */
+	uint32_t *present;     /* [3]: present[k] == epoch iff some chunk of class
+	                          k was deferred by this launch's fixed-shape kernel */
+	uint32_t epoch;        /* per-launch stamp (never 0) */
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
 };
 typedef struct ixg_kparams ixg_kparams;
 
 #define IXG_ZERO_PAGE 4096u
+
+/* deferred chunk classes: SHORT = every frame shorter than 112 bytes (the
+ * whole L4 segment lies in the 96-byte prefix + one 16-byte piece, no
+ * streaming), LONG = anything else */
+#define IXG_CLS_SHORT 1u
+#define IXG_CLS_LONG 2u
+#define IXG_SHORT_MAX 112u
 
 /* implemented in ixgrx_kernels.hip */
 /* enqueue one batch: the fixed-shape kernel (when p->defer) and the general

@@ -138,6 +138,43 @@ DEV uint32_t pick(const uint32_t (&d)[N], int idx) {
   return r;
 }
 
+// (m & x) | (~m & y): one v_bfi_b32 per dword
+DEV uint32_t bsel(uint32_t m, uint32_t x, uint32_t y) { return (m & x) | (~m & y); }
+DEV uint64_t bsel(uint32_t m, uint64_t x, uint64_t y) {
+  return (uint64_t)bsel(m, (uint32_t)(x >> 32), (uint32_t)(y >> 32)) << 32 | bsel(m, (uint32_t)x, (uint32_t)y);
+}
+
+// out[m] = v[s + m] (m < M) for a per-lane s in [0, 2^B): a log-depth mux.
+// Stage k (high bit first) picks a[i] or a[i + 2^k] on bit k of s, for the
+// entries later stages can still reach; indices past N read 0. Constant
+// indices, one all-ones/zero mask per stage (opaque to the compiler, which
+// otherwise rebuilds compare chains and spills lane masks) and v_bfi_b32:
+// no dynamic register indexing, no scratch.
+template <int B, int N, int M, typename T>
+DEV void window(const T (&v)[N], uint32_t s, T (&out)[M]) {
+  constexpr int W = M + (1 << B) - 1;
+  T a[W];
+#pragma unroll
+  for (int i = 0; i < W; i++) a[i] = i < N ? v[i < N ? i : 0] : T(0);
+#pragma unroll
+  for (int k = B - 1; k >= 0; k--) {
+    uint32_t m = 0u - ((s >> k) & 1u);
+    asm volatile("" : "+v"(m));
+    const int sh = 1 << k;
+#pragma unroll
+    for (int i = 0; i < M + sh - 1; i++) a[i] = bsel(m, a[i + sh], a[i]);
+  }
+#pragma unroll
+  for (int m = 0; m < M; m++) out[m] = a[m];
+}
+
+template <int B, int N, typename T>
+DEV T select(const T (&v)[N], uint32_t s) {
+  T o[1];
+  window<B, N, 1>(v, s, o);
+  return o[0];
+}
+
 // Sum of the bytes [a, e) of the prefix as 32-bit LE words, where a = 4*qa+2
 // (every region this path sums starts 2 bytes into a dword: the IPv4
 // header at 14, L4 headers at 14+4*ihl, IPv6 addresses at 22) and e >= a.
@@ -205,18 +242,33 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   const bool ip4 = etype == 0x0800u;
   const bool v6 = !FIXED && etype == 0x86DDu && (p.flags & IXG_F_IPV6);
 
-  // L4 header dwords: frame byte l4+b sits in dword q + (2+b)/4
+  // L4 header dwords: frame byte l4+b sits in dword q + (2+b)/4, where
+  // l4 = 4q + 2 (IPv4: q = 3 + max(ihl, 5); the IPv6 extension: L4 at 54,
+  // q = 13). The general shape reads them through a 4-stage mux.
   const int q = 3 + (ihl < 5 ? 5 : ihl);
-  uint32_t h0, h1, h3;
+  uint32_t h0, h1, h2, h3;
+  uint64_t C[kPrefixDw + 1];  // C[k] = sum of the 32-bit words of bytes [14, 4k)
+  uint64_t spre = 0;
   if (FIXED) {
-    h0 = d[8]; h1 = d[9]; h3 = d[11];
+    h0 = d[8]; h1 = d[9]; h2 = d[10]; h3 = d[11];
   } else {
-    h0 = pick<kPrefixDw, 8, 18>(d, q);
-    h1 = pick<kPrefixDw, 9, 19>(d, q + 1);
-    h3 = pick<kPrefixDw, 11, 21>(d, q + 3);
+    const uint32_t qs = v6 ? 5u : (uint32_t)(q - 8);  // in [0, 10]
+    uint32_t src4[kPrefixDw - 8], h[4];
+#pragma unroll
+    for (int j = 0; j < kPrefixDw - 8; j++) src4[j] = d[8 + j];
+    window<4>(src4, qs, h);
+    h0 = h[0]; h1 = h[1]; h2 = h[2]; h3 = h[3];
+    C[3] = 0;
+    C[4] = d[3] & 0xffff0000u;
+#pragma unroll
+    for (int k = 4; k < kPrefixDw; k++) C[k + 1] = C[k] + d[k];
+    // bytes [14, l4) = C[q] + the low half of dword q (= h0): the IPv4
+    // header, or the IPv6 header + the Ethernet type's successor bytes
+    uint64_t Cq[11];
+#pragma unroll
+    for (int j = 0; j < 11; j++) Cq[j] = C[8 + j];
+    spre = select<4>(Cq, qs) + (h0 & 0xffffu);
   }
-  // IPv6 extension: fixed offsets (L4 at 54 = dword 13 + 2)
-  if (v6) { h0 = d[13]; h1 = d[14]; h3 = d[16]; }
   const uint32_t b0 = (h0 >> 16) & 0xffu, b1 = h0 >> 24;                  // sport (wire)
   const uint32_t b2 = h1 & 0xffu, b3 = (h1 >> 8) & 0xffu;                 // dport (wire)
   const uint32_t w45 = h1 >> 16;                                          // L4 bytes 4,5 (LE)
@@ -237,7 +289,7 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
     if (FIXED) {
       hs = (uint64_t)(d[3] >> 16) + d[4] + d[5] + d[6] + d[7] + (d[8] & 0xffffu);
     } else {
-      hs = region_sum(d, 3, l4);
+      hs = spre;  // bytes [14, 14 + 4 ihl)
     }
     s.ip_res = (~fold16(hs)) & 0xffffu;                                    // chksum_internet
     s.flags |= IXG_RF_IP_CSUM_CHECKED | (s.ip_res == 0 ? IXG_RF_IP_CSUM_OK : 0u);
@@ -279,12 +331,10 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   uint32_t l4len = ip_len - 4u * (uint32_t)ihl;
   uint32_t seg_end = 14 + ip_len;
   bool seg_ok = ip4 && ver == 4 && ihl >= 5 && !frag && ip_len >= 4u * (uint32_t)ihl && seg_end <= L;
-  int qa = q;
   if (v6) {
     l4len = v6_plen;
     seg_end = 54 + v6_plen;
     seg_ok = v6_ok;
-    qa = 13;
   }
   s.l4 = v6 ? 54 : l4;
   s.l4len = l4len;
@@ -296,7 +346,7 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
 
   const uint32_t sp = s.proto;
   // UDP checksum field: L4 bytes 6,7 = low half of dword q+2
-  const uint32_t ucs = v6 ? 1u : ((FIXED ? d[10] : pick<kPrefixDw, 10, 20>(d, q + 2)) & 0xffffu);
+  const uint32_t ucs = v6 ? 1u : (h2 & 0xffffu);
   int kind = 0;
   if (seg_ok && ((sp == 6 && l4len >= 20) || (sp == 17 && l4len >= 8 && ucs != 0))) kind = 1;
   if (!v6 && seg_ok && sp == 1 && l4len >= 8) kind = 2;
@@ -304,14 +354,32 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   uint64_t acc = 0;
   if (kind) {
     const int e = (int)(seg_end < (uint32_t)(4 * NDW) ? seg_end : (uint32_t)(4 * NDW));
-    uint32_t dd[NDW];
+    if constexpr (FIXED) {
+      uint32_t dd[NDW];
 #pragma unroll
-    for (int j = 0; j < NDW; j++) dd[j] = d[j];
-    acc = region_sum(dd, FIXED ? 8 : qa, e);
+      for (int j = 0; j < NDW; j++) dd[j] = d[j];
+      acc = region_sum(dd, 8, e);
+    } else {
+      static_assert(FIXED || NDW == kPrefixDw, "the general shape sums the whole prefix");
+      // bytes [l4, e) = [14, e) - [14, l4); e >= l4 + 8 here
+      // (segments of at least 8 bytes), so e's dword index is in [10, 24]
+      const uint32_t qe = (uint32_t)e >> 2;
+      const uint32_t qi = (qe < 10u ? 10u : qe) - 10u;
+      uint64_t Ce[15];
+      uint32_t de[15];
+#pragma unroll
+      for (int j = 0; j < 15; j++) {
+        Ce[j] = C[10 + j];
+        de[j] = 10 + j < kPrefixDw ? d[10 + j < kPrefixDw ? 10 + j : 0] : 0u;
+      }
+      const uint64_t s_e = select<4>(Ce, qi) + (select<4>(de, qi) & ones(e & 3));
+      acc = s_e - spre;
+    }
     if (kind == 1) {
       uint64_t ps;
       if (v6) {
-        ps = region_sum(d, 5, 54);                      // src + dst (bytes 22..53)
+        // src + dst: bytes [22, 54) = [14, 54) - [14, 22)
+        ps = (C[13] + (d[13] & 0xffffu)) - (C[5] + (d[5] & 0xffffu));
       } else {
         ps = (uint64_t)(src & 0xffffu) + (src >> 16) + (dst & 0xffffu) + (dst >> 16);
       }
@@ -569,7 +637,9 @@ DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
   x.v96 = load16(short_tail, p.base + g.off + kStreamBase, p.zero + 16 * lane);
 }
 
-template <bool OFFS>
+// SHORT: every frame of the chunk is shorter than IXG_SHORT_MAX, so no
+// segment needs the streaming rounds (compiled out)
+template <bool OFFS, bool SHORT>
 DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x) {
   const uint32_t i = chunk * 64u + (uint32_t)lane;
@@ -593,10 +663,10 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   const bool strm = valid && s.stream;
   const uint32_t tail = s.seg_end - (uint32_t)kStreamBase;
   const uint32_t rr = tail & 15u, pend = (uint32_t)kStreamBase + (tail & ~15u);
-  const bool lng = strm && (pend > (uint32_t)kStreamBase || !short_tail);
+  const bool lng = !SHORT && strm && (pend > (uint32_t)kStreamBase || !short_tail);
   if (strm && !lng) s.l4_acc += piece_sum(v96, (int)rr);
-  const uint64_t m = __ballot(lng);
-  if (!m) {  // no long segment in this chunk (wave-uniform)
+  const uint64_t m = SHORT ? 0ull : __ballot(lng);
+  if (SHORT || !m) {  // no long segment in this chunk (wave-uniform)
     if (valid) {
       const uint32_t r4 = l4_residual(s);
       store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
@@ -691,8 +761,24 @@ DEV void fetch_prefix(const KParams& p, uint32_t chunk, int lane, uint32_t L, ui
   for (int k = 0; k < 3; k++) x.v[k] = *reinterpret_cast<const u32x4_a4*>(f + 16 + 16 * k);
 }
 
-DEV void fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, uint32_t L,
-                    const Prefix& x) {
+// a deferred chunk's class (ixgrx_internal.h): SHORT when no frame can need
+// the streaming rounds
+DEV uint32_t defer_class(bool valid, uint32_t L) {
+  return __all(!valid || L < IXG_SHORT_MAX) ? IXG_CLS_SHORT : IXG_CLS_LONG;
+}
+
+// Publish the classes a wave deferred (bit k = class k): one store per wave
+// and class, so the general kernels of an empty class exit at once.
+DEV void publish_classes(const KParams& p, uint32_t seen, int lane) {
+  if (lane == 0) {
+    if (seen & (1u << IXG_CLS_SHORT)) p.present[IXG_CLS_SHORT] = p.epoch;
+    if (seen & (1u << IXG_CLS_LONG)) p.present[IXG_CLS_LONG] = p.epoch;
+  }
+}
+
+// returns 1 << class for a deferred chunk, 0 when done here
+DEV uint32_t fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, uint32_t L,
+                        const Prefix& x) {
   const uint32_t i = chunk * 64u + (uint32_t)lane;
   const bool valid = i < p.n;
   uint32_t d[kPrefixDw];
@@ -713,9 +799,11 @@ DEV void fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t c
   const bool fast = !valid || (L <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
                                14 + ip_len <= 64);
   const bool all_fast = __all(fast);
-  if (lane == 0) p.defer[chunk] = all_fast ? 0 : 1;
-  if (!all_fast) return;
+  const uint32_t cls = all_fast ? 0u : defer_class(valid, L);
+  if (lane == 0) p.defer[chunk] = (uint8_t)cls;
+  if (!all_fast) return 1u << cls;
   process_fast(p, T, i, valid, L, d);
+  return 0;
 }
 
 }  // namespace
@@ -733,6 +821,7 @@ DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
   uint32_t Ld[AHEAD + 1];
   uint64_t od[AHEAD + 1];
   Prefix v[AHEAD];
+  uint32_t seen = 0;
 #pragma unroll
   for (int a = 0; a <= AHEAD; a++) fetch_desc<OFFS>(p, c + a * nw, lane, Ld[a], od[a]);
 #pragma unroll
@@ -744,7 +833,7 @@ DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
     fetch_desc<OFFS>(p, c + (AHEAD + 1) * nw, lane, Ln, on);
     Prefix vn;
     fetch_prefix(p, c + AHEAD * nw, lane, Ld[AHEAD], od[AHEAD], vn);
-    fast_chunk(p, T, c, lane, Ld[0], v[0]);
+    seen |= fast_chunk(p, T, c, lane, Ld[0], v[0]);
     c += nw;
     if (c >= nchunks) break;
 #pragma unroll
@@ -758,6 +847,7 @@ DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
     for (int a = 0; a + 1 < AHEAD; a++) v[a] = v[a + 1];
     v[AHEAD - 1] = vn;
   }
+  publish_classes(p, seen, lane);
 }
 
 #define IXG_FAST_KERNEL(NAME, OFFS, AHEAD, WAVES)                                    \
@@ -819,7 +909,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   const uint64_t lim = (uint64_t)(p.n - 1) * p.stride + p.len[p.n - 1] + IXG_TAIL_PAD;
   const uint32_t fw = (uint32_t)lane * (p.stride >> 2);  // this lane's frame, in dwords
   u32x4 cur[4];
-  uint32_t Lc;
+  uint32_t Lc, seen = 0;
   fastc_issue(p, c, nchunks, lim, lane, cur, Lc);
   for (;;) {
     const uint32_t cn = c + nw;
@@ -854,7 +944,9 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     const bool fast = !valid || (Lc <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
                                  14 + ip_len <= 64);
     const bool all_fast = __all(fast);
-    if (lane == 0) p.defer[c] = all_fast ? 0 : 1;
+    const uint32_t cls = all_fast ? 0u : defer_class(valid, Lc);
+    if (lane == 0) p.defer[c] = (uint8_t)cls;
+    seen |= (1u << cls) & ~1u;
     if (all_fast) process_fast(p, T, i, valid, Lc, d);
     // the next iteration's LDS writes must not pass this one's reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -866,6 +958,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     for (int k = 0; k < 4; k++) cur[k] = nxt[k];
     Lc = Ln;
   }
+  publish_classes(p, seen, lane);
 }
 
 extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
@@ -882,7 +975,7 @@ ixg_rx_fastc_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY>
+template <bool OFFS, bool EARLY, bool SHORT>
 DEV void gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
@@ -896,7 +989,7 @@ DEV void gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     gen_desc<OFFS>(p, c2, lane, D2);
     GPre P1;
     if (EARLY) gen_pre(p, D1, lane, P1);
-    general_chunk<OFFS>(p, T, c0, lane, w, D0, P0);
+    general_chunk<OFFS, SHORT>(p, T, c0, lane, w, D0, P0);
     if (!EARLY) gen_pre(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
@@ -906,7 +999,10 @@ DEV void gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
   }
 }
 
-template <bool OFFS>
+// CLS: the deferred class this kernel takes (IXG_CLS_SHORT: no streaming
+// code at all, so fewer registers and more waves; IXG_CLS_LONG: everything,
+// and every chunk when p.defer is null).
+template <bool OFFS, uint32_t CLS, bool SEARLY = true>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -917,10 +1013,11 @@ DEV void general_body(const KParams& p) {
   const uint32_t ngroups = (nchunks + 63u) >> 6;
   // a block with no deferred chunk exits before staging the tables (the
   // common case behind the fixed-shape kernel: 64 B frames)
+  if (p.defer && p.present[CLS] != p.epoch) return;  // nothing of this class deferred
   bool any = p.defer == nullptr;
   for (uint32_t g = blockIdx.x * kWaves + wave; !any && g < ngroups; g += nw) {
     const uint32_t ci = g * 64u + (uint32_t)lane;
-    any = __ballot(ci < nchunks && p.defer[ci] != 0) != 0;
+    any = __ballot(ci < nchunks && p.defer[ci] == CLS) != 0;
   }
   if (!__syncthreads_or(any)) return;
   // IPv6 Toeplitz table (36 KiB, dynamic LDS: present only with IXG_F_IPV6)
@@ -940,7 +1037,7 @@ DEV void general_body(const KParams& p) {
     for (int k = 0; k < kQGroups; k++) {
       const uint32_t g = g0 + (uint32_t)k * nw;
       const uint32_t ci = g * 64u + (uint32_t)lane;
-      const bool want = g < ngroups && ci < nchunks && (p.defer == nullptr || p.defer[ci] != 0);
+      const bool want = g < ngroups && ci < nchunks && (p.defer == nullptr || p.defer[ci] == CLS);
       const uint64_t m = __ballot(want);
       if (want) q[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
       nq += (uint32_t)__popcll(m);
@@ -953,24 +1050,34 @@ DEV void general_body(const KParams& p) {
     // chunk, as two separate loops, so no load in either is conditional.
     GDesc D0;
     gen_desc<OFFS>(p, q[0], lane, D0);
-    if (__any(D0.L > (uint32_t)kStreamBase + 32u))
-      gen_walk<OFFS, false>(p, T, w, q, nq, lane, D0);
+    if (CLS == IXG_CLS_SHORT)
+      gen_walk<OFFS, SEARLY, true>(p, T, w, q, nq, lane, D0);
+    else if (__any(D0.L > (uint32_t)kStreamBase + 32u))
+      gen_walk<OFFS, false, false>(p, T, w, q, nq, lane, D0);
     else
-      gen_walk<OFFS, true>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, true, false>(p, T, w, q, nq, lane, D0);
     __builtin_amdgcn_wave_barrier();
   }
 }
 
-#define IXG_GEN_KERNEL(NAME, OFFS, WAVES)                                                           \
+#define IXG_GEN_KERNEL(NAME, OFFS, CLS, WAVES, ...)                                                 \
   extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
-  NAME(KParams p) { general_body<OFFS>(p); }
+  NAME(KParams p) { general_body<OFFS, CLS, ##__VA_ARGS__>(p); }
 // variants for A/B (IXGRX_GEN_VARIANT); index 0 is the default
-IXG_GEN_KERNEL(ixg_rx_general_s, false, 2)
-IXG_GEN_KERNEL(ixg_rx_general_o, true, 2)
-IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, 3)
-IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, 3)
-IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, 4)
-IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, 4)
+IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2)
+IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
+IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
+IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
+IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, IXG_CLS_LONG, 4)
+// the short-class general kernel (no streaming rounds); variants for A/B
+// (IXGRX_SHORT_VARIANT), index 0 the default
+IXG_GEN_KERNEL(ixg_rx_short_s, false, IXG_CLS_SHORT, 3)
+IXG_GEN_KERNEL(ixg_rx_short_o, true, IXG_CLS_SHORT, 3)
+IXG_GEN_KERNEL(ixg_rx_short_w4_s, false, IXG_CLS_SHORT, 4)
+IXG_GEN_KERNEL(ixg_rx_short_w4_o, true, IXG_CLS_SHORT, 4)
+IXG_GEN_KERNEL(ixg_rx_short_late_s, false, IXG_CLS_SHORT, 4, false)
+IXG_GEN_KERNEL(ixg_rx_short_late_o, true, IXG_CLS_SHORT, 4, false)
 
 typedef void (*kern_fn)(KParams);
 // [variant][layout: 0 = stride, 1 = offsets]
@@ -981,6 +1088,10 @@ static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
 static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
                                    {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
                                    {ixg_rx_general_w4_s, ixg_rx_general_w4_o}};
+static const kern_fn k_short[][2] = {{ixg_rx_short_s, ixg_rx_short_o},
+                                     {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
+                                     {ixg_rx_short_late_s, ixg_rx_short_late_o}};
+static const int k_nshort = sizeof(k_short) / sizeof(k_short[0]);
 static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
 static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
 
@@ -1009,14 +1120,15 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
   return g ? (uint32_t)g : 1u;
 }
 
-// variant = fast_variant | (general_variant << 8). Fast variant 0 picks the
+// variant = fast_variant | (general_variant << 8) | (short_variant << 16). Fast variant 0 picks the
 // coalesced kernel for fixed strides <= 64 B (16-B aligned base), else the
 // lane-load kernel; 1..3 force the lane-load A/B builds; 4 forces variant
 // 0's lane-load kernel.
 extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
-  int fv = variant & 0xff, gv = (variant >> 8) & 0xff;
+  int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff;
   if (gv >= k_ngen) gv = 0;
+  if (sv >= k_nshort) sv = 0;
   const int lay = p.off ? 1 : 0;
   const uint64_t nchunks = ((uint64_t)p.n + 63u) / 64u;
   const uint64_t wave_blocks = (nchunks + kWaves - 1) / kWaves;              // one wave per chunk
@@ -1033,8 +1145,12 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     }
     hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, ncu)), dim3(kBlock), 0, (hipStream_t)stream, p);
   }
-  const kern_fn kg = k_gen[gv][lay];
   const size_t sh6 = p.tab6 ? 36u * 256u * sizeof(uint32_t) : 0u;
+  if (p.defer) {
+    const kern_fn ks = k_short[sv][lay];
+    hipLaunchKernelGGL(ks, dim3(grid_for(ks, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
+  }
+  const kern_fn kg = k_gen[gv][lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }

@@ -32,20 +32,25 @@ def main():
     engs = {}
     for v in args.variants.split(","):
         # "3" = fast variant 3; "0:1" = fast variant 0 + general variant 1;
-        # "g1" = general-only with general variant 1
+        # "0:0:2" = + short variant 2; "g1" = general-only with general variant 1
         os.environ["IXGRX_FORCE_GENERAL"] = "1" if v.startswith("g") else "0"
-        fv, _, gv = (("0", "", v[1:] or "0") if v.startswith("g") else v.partition(":"))
-        os.environ["IXGRX_FAST_VARIANT"] = fv
-        os.environ["IXGRX_GEN_VARIANT"] = gv or "0"
+        parts = (["0", v[1:] or "0"] if v.startswith("g") else v.split(":")) + ["0", "0"]
+        os.environ["IXGRX_FAST_VARIANT"] = parts[0] or "0"
+        os.environ["IXGRX_GEN_VARIANT"] = parts[1] or "0"
+        os.environ["IXGRX_SHORT_VARIANT"] = parts[2] or "0"
         engs[v] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags))
     s = torch.cuda.current_stream()
     times = {v: [] for v in engs}
-    ok = {}
+    # parity: every variant's records equal the first variant's, and each
+    # tiled batch is self-consistent (the oracle checks the kernels in tests/)
+    ok, first = {}, None
     for v, e in engs.items():  # warm + parity
         for _ in range(3):
             wl.launch(e, s.cuda_stream)
         torch.cuda.synchronize()
-        ok[v] = wl.check(traces.RSS_KEY)
+        tiled, rec = wl.snapshot()
+        first = rec if first is None else first
+        ok[v] = bool(tiled and np.array_equal(rec, first))
     for _ in range(args.rounds):
         for v, e in engs.items():
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.k)]
