@@ -45,6 +45,8 @@ WORKLOADS = {
     "c4": ("tcp1514", 8 * 1024 * 1024, 1 << 13, "C4 per-GPU shard: 8M x 1514B IPv4/TCP frames (stride 1516)"),
     "c3": ("imix", 16 * 1024 * 1024, 1 << 18, "C3: 16M IMIX 7:4:1 (60/590/1514B) TCP+UDP, packed, u64 offsets"),
     "c5": ("mixed", 16 * 1024 * 1024, 1 << 18, "C5: 16M mixed IPv4 ihl 5..15 + 50% IPv6, packed"),
+    # A/B only (not a config): C2's frames in the packed u64-offset layout
+    "c2o": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2 frames, u64-offset layout (A/B only)"),
 }
 
 
@@ -76,6 +78,9 @@ class Workload:
         assert self.n % pool == 0
         self.reps = self.n // pool
         self.pool = traces.make_trace(kind, pool, seed=seed)
+        if name == "c2o":
+            tr = self.pool
+            self.pool = traces.Trace(tr.blob, tr.offsets().copy(), tr.len, 0)
         self.flags = 2 if kind == "mixed" else 0
         tr = self.pool
         self.bytes_per_pkt = float(alg_bytes(tr).mean())

@@ -30,8 +30,10 @@ struct ixg_kparams {
 	                          kernel, IXG_CLS_SHORT / IXG_CLS_LONG = left for
 	                          that general kernel; NULL = the long general
 	                          kernel does everything */
-	uint32_t *present;     /* [3]: present[k] == epoch iff some chunk of class
-	                          k was deferred by this launch's fixed-shape kernel */
+	uint32_t *present;     /* [4]: present[k] == epoch (k = 1, 2) iff some chunk
+	                          of class k was deferred in this launch;
+	                          present[0] == epoch iff the sampler ran, and
+	                          then present[3] is the launch's IXG_MODE_* */
 	uint32_t epoch;        /* per-launch stamp (never 0) */
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
@@ -46,6 +48,16 @@ typedef struct ixg_kparams ixg_kparams;
 #define IXG_CLS_SHORT 1u
 #define IXG_CLS_LONG 2u
 #define IXG_SHORT_MAX 112u
+
+/* how a launch splits the work, chosen on the device by the sampler kernel
+ * from the lengths of up to 64 evenly spread chunks (u64-offset batches and
+ * strides > 64 B; coalesced fixed-stride batches are always FAST):
+ * FAST  = the fixed-shape kernel first, then deferred short / long chunks;
+ * SHORT = the short kernel walks every chunk, deferring long ones;
+ * LONG  = the long kernel walks every chunk. */
+#define IXG_MODE_FAST 0u
+#define IXG_MODE_SHORT 1u
+#define IXG_MODE_LONG 2u
 
 /* implemented in ixgrx_kernels.hip */
 /* enqueue one batch: the fixed-shape kernel (when p->defer) and the general

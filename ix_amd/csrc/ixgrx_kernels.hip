@@ -631,20 +631,34 @@ DEV void gen_desc(const KParams& p, uint32_t chunk, int lane, GDesc& g) {
 
 // every load is issued (zero page / dummy when there is nothing to read), so
 // hipcc's vmcnt accounting stays exact across the pipeline
+// GATE: load nothing for a chunk with a frame of IXG_SHORT_MAX bytes or more
+// (the short-first pass leaves such chunks to the long kernel)
+template <bool GATE = false>
 DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
-  load_prefix<0, 6>(p.base + g.off, g.L, reinterpret_cast<const uint8_t*>(p.tab), x.d);
+  const uint32_t Lg = (!GATE || __all(g.L < IXG_SHORT_MAX)) ? g.L : 0u;
+  load_prefix<0, 6>(p.base + g.off, Lg, reinterpret_cast<const uint8_t*>(p.tab), x.d);
   const bool short_tail = g.L > (uint32_t)kStreamBase && g.L < (uint32_t)kStreamBase + 32u;
   x.v96 = load16(short_tail, p.base + g.off + kStreamBase, p.zero + 16 * lane);
 }
 
-// SHORT: every frame of the chunk is shorter than IXG_SHORT_MAX, so no
-// segment needs the streaming rounds (compiled out)
-template <bool OFFS, bool SHORT>
-DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
+// MODE: kModeLong: any chunk; kModeFirst (the short kernel): the chunk's
+// class is checked here, a chunk with a frame of IXG_SHORT_MAX bytes or more
+// is flagged for the long kernel, and for the others no segment needs the
+// streaming rounds (compiled out). Returns true when the chunk was deferred.
+constexpr int kModeLong = 0, kModeFirst = 2;
+
+template <bool OFFS, int MODE>
+DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x) {
+  constexpr bool SHORT = MODE != kModeLong;
   const uint32_t i = chunk * 64u + (uint32_t)lane;
   const bool valid = i < p.n;
   const uint32_t L = g.L;
+  if (MODE == kModeFirst) {
+    const bool defer = !__all(L < IXG_SHORT_MAX);  // L = 0 past the end
+    if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
+    if (defer) return true;
+  }
   const uint64_t off = g.off;
   const uint32_t (&d)[kPrefixDw] = x.d;
   const u32x4& v96 = x.v96;
@@ -671,7 +685,7 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
       const uint32_t r4 = l4_residual(s);
       store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
     }
-    return;
+    return false;
   }
   // records for both outcomes of the pending L4 check; then only these
   // few registers stay live across the streaming rounds
@@ -713,6 +727,7 @@ DEV void general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
       store_record(p, i, rok, ip_res, r4);
     }
   }
+  return false;
 }
 
 // stage the hash tables (24 KiB) once per persistent workgroup
@@ -776,6 +791,11 @@ DEV void publish_classes(const KParams& p, uint32_t seen, int lane) {
   }
 }
 
+// the launch's IXG_MODE_* (FAST when the sampler did not run)
+DEV uint32_t launch_mode(const KParams& p) {
+  return (p.defer && p.present[0] == p.epoch) ? p.present[3] : IXG_MODE_FAST;
+}
+
 // returns 1 << class for a deferred chunk, 0 when done here
 DEV uint32_t fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, uint32_t L,
                         const Prefix& x) {
@@ -817,7 +837,7 @@ DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
   uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (c >= nchunks) return;
+  if (c >= nchunks || launch_mode(p) != IXG_MODE_FAST) return;
   uint32_t Ld[AHEAD + 1];
   uint64_t od[AHEAD + 1];
   Prefix v[AHEAD];
@@ -975,33 +995,38 @@ ixg_rx_fastc_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, bool SHORT>
-DEV void gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
+template <bool OFFS, bool EARLY, int MODE>
+DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
+  constexpr bool GATE = MODE == kModeFirst;
+  bool deferred = false;
   uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
   GDesc D1;
   gen_desc<OFFS>(p, c1, lane, D1);
   GPre P0;
-  gen_pre(p, D0, lane, P0);
+  gen_pre<GATE>(p, D0, lane, P0);
   for (uint32_t j = 0; j < nq; j++) {
     const uint32_t c2 = j + 2 < nq ? q[j + 2] : kNoChunk;
     GDesc D2;
     gen_desc<OFFS>(p, c2, lane, D2);
     GPre P1;
-    if (EARLY) gen_pre(p, D1, lane, P1);
-    general_chunk<OFFS, SHORT>(p, T, c0, lane, w, D0, P0);
-    if (!EARLY) gen_pre(p, D1, lane, P1);
+    if (EARLY) gen_pre<GATE>(p, D1, lane, P1);
+    deferred |= general_chunk<OFFS, MODE>(p, T, c0, lane, w, D0, P0);
+    if (!EARLY) gen_pre<GATE>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
     D0 = D1;
     D1 = D2;
     P0 = P1;
   }
+  return deferred;
 }
 
-// CLS: the deferred class this kernel takes (IXG_CLS_SHORT: no streaming
-// code at all, so fewer registers and more waves; IXG_CLS_LONG: everything,
-// and every chunk when p.defer is null).
+// CLS: the class this kernel takes. IXG_CLS_SHORT: no streaming code at
+// all, so fewer registers and more waves; it takes the chunks the
+// fixed-shape kernel deferred as short or, in IXG_MODE_SHORT, walks every
+// chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
+// deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
 template <bool OFFS, uint32_t CLS, bool SEARLY = true>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
@@ -1013,8 +1038,10 @@ DEV void general_body(const KParams& p) {
   const uint32_t ngroups = (nchunks + 63u) >> 6;
   // a block with no deferred chunk exits before staging the tables (the
   // common case behind the fixed-shape kernel: 64 B frames)
-  if (p.defer && p.present[CLS] != p.epoch) return;  // nothing of this class deferred
-  bool any = p.defer == nullptr;
+  const uint32_t mode = launch_mode(p);
+  const bool all = CLS == IXG_CLS_SHORT ? mode == IXG_MODE_SHORT : (p.defer == nullptr || mode == IXG_MODE_LONG);
+  if (!all && p.present[CLS] != p.epoch) return;  // nothing of this class deferred
+  bool any = all;
   for (uint32_t g = blockIdx.x * kWaves + wave; !any && g < ngroups; g += nw) {
     const uint32_t ci = g * 64u + (uint32_t)lane;
     any = __ballot(ci < nchunks && p.defer[ci] == CLS) != 0;
@@ -1029,6 +1056,7 @@ DEV void general_body(const KParams& p) {
   const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
                   LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6)};
   lds_u32* q = LDS(lds_u32, sh_q[wave]);
+  bool seen = false;
   // groups g0, g0+nw, ... of this wave, kQGroups at a time: their deferred
   // chunk ids go to an LDS list, which the pipeline then walks
   for (uint32_t g0 = blockIdx.x * kWaves + wave; g0 < ngroups; g0 += kQGroups * nw) {
@@ -1037,7 +1065,7 @@ DEV void general_body(const KParams& p) {
     for (int k = 0; k < kQGroups; k++) {
       const uint32_t g = g0 + (uint32_t)k * nw;
       const uint32_t ci = g * 64u + (uint32_t)lane;
-      const bool want = g < ngroups && ci < nchunks && (p.defer == nullptr || p.defer[ci] == CLS);
+      const bool want = g < ngroups && ci < nchunks && (all || p.defer[ci] == CLS);
       const uint64_t m = __ballot(want);
       if (want) q[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
       nq += (uint32_t)__popcll(m);
@@ -1051,13 +1079,14 @@ DEV void general_body(const KParams& p) {
     GDesc D0;
     gen_desc<OFFS>(p, q[0], lane, D0);
     if (CLS == IXG_CLS_SHORT)
-      gen_walk<OFFS, SEARLY, true>(p, T, w, q, nq, lane, D0);
+      seen |= gen_walk<OFFS, SEARLY, kModeFirst>(p, T, w, q, nq, lane, D0);
     else if (__any(D0.L > (uint32_t)kStreamBase + 32u))
-      gen_walk<OFFS, false, false>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, false, kModeLong>(p, T, w, q, nq, lane, D0);
     else
-      gen_walk<OFFS, true, false>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, true, kModeLong>(p, T, w, q, nq, lane, D0);
     __builtin_amdgcn_wave_barrier();
   }
+  if (CLS == IXG_CLS_SHORT) publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
 }
 
 #define IXG_GEN_KERNEL(NAME, OFFS, CLS, WAVES, ...)                                                 \
@@ -1078,6 +1107,37 @@ IXG_GEN_KERNEL(ixg_rx_short_w4_s, false, IXG_CLS_SHORT, 4)
 IXG_GEN_KERNEL(ixg_rx_short_w4_o, true, IXG_CLS_SHORT, 4)
 IXG_GEN_KERNEL(ixg_rx_short_late_s, false, IXG_CLS_SHORT, 4, false)
 IXG_GEN_KERNEL(ixg_rx_short_late_o, true, IXG_CLS_SHORT, 4, false)
+
+// The sampler: one block reads the lengths of up to 64 evenly spread chunks
+// and picks the launch's IXG_MODE_* (ixgrx_internal.h): FAST when at least
+// half of them could be fixed-shape by length (every frame <= 64 B), else
+// SHORT when at least half are short, else LONG.
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
+  __shared__ uint32_t cnt[2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t ns = nchunks < 64u ? nchunks : 64u;
+  uint32_t nf = 0, nsh = 0;
+  for (uint32_t k = (uint32_t)wave; k < ns; k += kWaves) {
+    const uint32_t c = (uint32_t)((uint64_t)k * nchunks / ns);
+    const uint32_t i = c * 64u + (uint32_t)lane;
+    const uint32_t L = i < p.n ? p.len[i] : 0u;
+    nf += __all(L <= 64u) ? 1u : 0u;
+    nsh += __all(L < IXG_SHORT_MAX) ? 1u : 0u;
+  }
+  if (lane == 0) {
+    atomicAdd(&cnt[0], nf);
+    atomicAdd(&cnt[1], nsh);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t mode = 2 * cnt[0] >= ns ? IXG_MODE_FAST : (2 * cnt[1] >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
+    p.present[3] = mode;
+    p.present[0] = p.epoch;
+  }
+}
 
 typedef void (*kern_fn)(KParams);
 // [variant][layout: 0 = stride, 1 = offsets]
@@ -1133,19 +1193,21 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   const uint64_t nchunks = ((uint64_t)p.n + 63u) / 64u;
   const uint64_t wave_blocks = (nchunks + kWaves - 1) / kWaves;              // one wave per chunk
   const uint64_t group_blocks = ((nchunks + 63u) / 64u + kWaves - 1) / kWaves; // one wave per 64 chunks
-  if (p.defer) {
-    const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&
+  const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&
                       (reinterpret_cast<uintptr_t>(p.base) & 15u) == 0u;
+  const size_t sh6 = p.tab6 ? 36u * 256u * sizeof(uint32_t) : 0u;
+  if (p.defer) {
     kern_fn kf;
     if (fv == 0 && coal) {
       kf = ixg_rx_fastc_s;
     } else {
+      // fast variant 5: no sampler (the fixed-shape kernel always runs first)
+      if (fv != 5) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
       if (fv >= k_nfast) fv = 0;
       kf = k_fast[fv][lay];
     }
     hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, ncu)), dim3(kBlock), 0, (hipStream_t)stream, p);
   }
-  const size_t sh6 = p.tab6 ? 36u * 256u * sizeof(uint32_t) : 0u;
   if (p.defer) {
     const kern_fn ks = k_short[sv][lay];
     hipLaunchKernelGGL(ks, dim3(grid_for(ks, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
