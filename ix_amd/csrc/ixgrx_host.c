@@ -23,6 +23,7 @@ struct ixg_ctx {
 	uint32_t ncu;        /* compute units: persistent grids are sized from it */
 	int force_general;   /* IXGRX_FORCE_GENERAL=1: skip the fixed-shape kernel (tests/A-B) */
 	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
+	uint32_t force_mode; /* IXGRX_MODE=fast|short|long: force the launch split (tests) */
 	uint8_t *d_defer;    /* one flag per 64-packet chunk */
 	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
 	uint32_t *d_present; /* [3] per-class stamps (ixg_kparams.present) */
@@ -210,6 +211,14 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		c->fast_variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
 		e = getenv("IXGRX_SHORT_VARIANT");
 		c->fast_variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
+		e = getenv("IXGRX_MODE");
+		c->force_mode = IXG_MODE_AUTO;
+		if (e && !strcmp(e, "fast"))
+			c->force_mode = IXG_MODE_FAST;
+		else if (e && !strcmp(e, "short"))
+			c->force_mode = IXG_MODE_SHORT;
+		else if (e && !strcmp(e, "long"))
+			c->force_mode = IXG_MODE_LONG;
 	}
 	c->ncu = (uint32_t)prop.multiProcessorCount;
 	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
@@ -289,6 +298,7 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 		if (++c->epoch == 0)
 			c->epoch = 1;
 		p.epoch = c->epoch;
+		p.force_mode = c->force_mode;
 	}
 	return ixgrx_launch(&p, c->fast_variant, c->ncu, s) == 0 ? 0 : -EIO;
 }

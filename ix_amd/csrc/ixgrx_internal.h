@@ -35,6 +35,8 @@ struct ixg_kparams {
 	                          present[0] == epoch iff the sampler ran, and
 	                          then present[3] is the launch's IXG_MODE_* */
 	uint32_t epoch;        /* per-launch stamp (never 0) */
+	uint32_t force_mode;   /* IXG_MODE_* for the sampler to write instead of
+	                          sampling (tests), or IXG_MODE_AUTO */
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
 };
@@ -58,6 +60,7 @@ typedef struct ixg_kparams ixg_kparams;
 #define IXG_MODE_FAST 0u
 #define IXG_MODE_SHORT 1u
 #define IXG_MODE_LONG 2u
+#define IXG_MODE_AUTO 0xffffffffu
 
 /* implemented in ixgrx_kernels.hip */
 /* enqueue one batch: the fixed-shape kernel (when p->defer) and the general

@@ -1133,7 +1133,8 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t mode = 2 * cnt[0] >= ns ? IXG_MODE_FAST : (2 * cnt[1] >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
+    uint32_t mode = 2 * cnt[0] >= ns ? IXG_MODE_FAST : (2 * cnt[1] >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
+    if (p.force_mode != IXG_MODE_AUTO) mode = p.force_mode;
     p.present[3] = mode;
     p.present[0] = p.epoch;
   }
@@ -1197,16 +1198,20 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
                       (reinterpret_cast<uintptr_t>(p.base) & 15u) == 0u;
   const size_t sh6 = p.tab6 ? 36u * 256u * sizeof(uint32_t) : 0u;
   if (p.defer) {
-    kern_fn kf;
+    kern_fn kf = nullptr;
+    const bool forced = p.force_mode != IXG_MODE_AUTO;
     if (fv == 0 && coal) {
-      kf = ixg_rx_fastc_s;
+      // coalesced fixed stride: always fixed-shape first (no sampler),
+      // unless a test forces another split
+      if (forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
+      if (!forced || p.force_mode == IXG_MODE_FAST) kf = ixg_rx_fastc_s;
     } else {
       // fast variant 5: no sampler (the fixed-shape kernel always runs first)
-      if (fv != 5) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
+      if (fv != 5 || forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
       if (fv >= k_nfast) fv = 0;
       kf = k_fast[fv][lay];
     }
-    hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, ncu)), dim3(kBlock), 0, (hipStream_t)stream, p);
+    if (kf) hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, ncu)), dim3(kBlock), 0, (hipStream_t)stream, p);
   }
   if (p.defer) {
     const kern_fn ks = k_short[sv][lay];

@@ -34,24 +34,29 @@ def _diff(got, exp, what):
                           f"gpu {g[bad[0]].tolist()} vs exp {exp[bad[0]].tolist()}"
 
 
-@pytest.fixture(scope="module", params=["auto", "general"])
+@pytest.fixture(scope="module", params=["auto", "general", "fast", "short", "long"])
 def engines(request):
-    """Engines on the default path (fixed-shape kernel + general kernel for
-    flagged chunks) and with IXGRX_FORCE_GENERAL=1 (general kernel only)."""
+    """Engines on the default path (the device-side sampler picks the split),
+    with IXGRX_FORCE_GENERAL=1 (general kernel only, no defer flags), and
+    with each launch split forced (IXGRX_MODE): fixed-shape kernel first,
+    short kernel walking every chunk, long kernel walking every chunk."""
     cache = {}
+    env = {"IXGRX_FORCE_GENERAL": "1" if request.param == "general" else "0",
+           "IXGRX_MODE": request.param if request.param in ("fast", "short", "long") else "auto"}
 
     def get(key=KEY, nb=128, dev=0, flags=0):
         k = (bytes(key), nb, dev, flags)
         if k not in cache:
-            old = os.environ.get("IXGRX_FORCE_GENERAL")
-            os.environ["IXGRX_FORCE_GENERAL"] = "1" if request.param == "general" else "0"
+            old = {v: os.environ.get(v) for v in env}
+            os.environ.update(env)
             try:
                 cache[k] = ixgrx.RxEngine(ixgrx.Config(bytes(key), nb, dev, flags))
             finally:
-                if old is None:
-                    del os.environ["IXGRX_FORCE_GENERAL"]
-                else:
-                    os.environ["IXGRX_FORCE_GENERAL"] = old
+                for v, o in old.items():
+                    if o is None:
+                        del os.environ[v]
+                    else:
+                        os.environ[v] = o
         return cache[k]
     yield get
     for e in cache.values():
