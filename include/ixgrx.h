@@ -274,6 +274,65 @@ int ixg_demux_batch_host(void *ctx, const void *frames, const uint64_t *off, con
 			 uint32_t stride, uint32_t n, const struct ixg_rx_rec *rec,
 			 struct ixg_demux_rec *out);
 
+/* ---- TX: header build + checksums, the mirror transform ---- */
+
+/* One outgoing segment, as the reference's two TX paths receive it:
+ *  - proto 6: tcp_output_packet (dp/net/tcp_api.c:773-826) gets a pbuf chain
+ *    holding the TCP header lwIP built + payload (seg bytes here), and the
+ *    pcb's local/remote IP, tos and ttl;
+ *  - proto 17: udp_output (dp/net/udp.c:102-130) gets the payload (seg bytes)
+ *    and an ip_tuple {dst_ip, src_port, dst_port}; the source IP is
+ *    CFG.host_addr, tos 0 and ttl 64 (ip_setup_header, dp/net/net.h:65-78).
+ * The Ethernet header is ip_send_one's (dp/net/ip.c:192-219): dhost = the
+ * ARP entry of the next hop (here dmac[dmac_idx] of the MAC table), shost =
+ * CFG.mac, type 0x0800. */
+struct ixg_tx_seg {
+	uint64_t seg_off;   /* device byte offset of the segment bytes, 4-aligned */
+	uint64_t out_off;   /* frame start in the output buffer, 16-aligned */
+	uint32_t src_ip;    /* raw, network byte order (pcb->local_ip.addr) */
+	uint32_t dst_ip;    /* raw, network byte order */
+	uint16_t seg_len;   /* TCP: header + payload; UDP: payload (<= 1472) */
+	uint16_t src_port;  /* UDP: host order (ip_tuple); TCP: unused */
+	uint16_t dst_port;  /* UDP: host order; TCP: unused */
+	uint8_t proto;      /* 6 or 17 */
+	uint8_t tos;
+	uint8_t ttl;
+	uint8_t rsvd;
+	uint16_t dmac_idx;  /* index into the context's destination MAC table */
+	uint32_t rsvd2;
+};
+
+/* flags of ixg_tx_batch_dev */
+#define IXG_TX_OFFLOAD (1u << 0) /* leave a TCP frame's checksums as IX leaves
+                                    them for the NIC (PKT_TX_IP_CKSUM |
+                                    PKT_TX_TCP_CKSUM, tcp_api.c:815-817): IP
+                                    checksum 0 and the TCP checksum field =
+                                    inet_chksum_pseudo's seed
+                                    (dp/lwip/inet_chksum.c:323-360). Default:
+                                    both computed, as the NIC puts them on
+                                    the wire. UDP is the same in both: IP
+                                    checksum by chksum_internet (udp.c:121),
+                                    UDP checksum 0 (udp.c:127). */
+
+/* The MAC addresses: src = CFG.mac, dmacs = n_dmac next-hop addresses (the
+ * ARP table rows segments refer to by dmac_idx). 0 or -errno. */
+int ixg_tx_set_macs(void *ctx, const uint8_t src_mac[6], const uint8_t *dmacs, uint32_t n_dmac);
+
+/* Build n frames: frame i = Ethernet + IPv4 (+ UDP) header + the segment
+ * bytes, written at out + segs[i].out_off, with out_len[i] = its length
+ * (14 + 20 + seg_len, + 8 for UDP). Bytes from the frame end up to the next
+ * 16-byte boundary may be overwritten. segs, seg_buf, out, out_len are
+ * device pointers. Asynchronous on `stream`. 0 or -errno (-EINVAL: bad
+ * proto/length/alignment is reported per frame as out_len 0). */
+int ixg_tx_batch_dev(void *ctx, const void *seg_buf, const struct ixg_tx_seg *segs, uint32_t n, void *out,
+		     uint16_t *out_len, uint32_t flags, void *stream);
+
+/* Host variant: host seg_buf (seg_buf_len bytes), host segs, host out
+ * (large enough for every out_off + round_up(frame, 16)), host out_len.
+ * Synchronous. */
+int ixg_tx_batch_host(void *ctx, const void *seg_buf, size_t seg_buf_len, const struct ixg_tx_seg *segs,
+		      uint32_t n, void *out, size_t out_size, uint16_t *out_len, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

@@ -15,6 +15,7 @@
 #include "../../include/ixgrx.h"
 #include "ixgrx_internal.h"
 #include "ixgrx_demux.h"
+#include "ixgrx_tx.h"
 
 struct ixg_ctx {
 	int device;
@@ -53,6 +54,15 @@ struct ixg_ctx {
 	struct ixg_listen_key *d_listen;
 	struct ixg_demux_rec *d_dmx; /* host-path output staging */
 	size_t d_dmx_cap;
+	/* TX (ixg_tx_set_macs) */
+	uint32_t *d_dmacs;           /* rows of 2 dwords */
+	uint32_t n_dmac;
+	uint32_t smac_lo, smac_hi;
+	uint8_t *d_txbuf, *d_txout;  /* host-path staging */
+	size_t d_txbuf_cap, d_txout_cap;
+	struct ixg_tx_seg *d_txsegs;
+	uint16_t *d_txlen;
+	size_t d_txn_cap;
 };
 
 /* ---- hash tables -------------------------------------------------------- */
@@ -133,7 +143,7 @@ const char *ixg_strerror(int err)
 	case -ENOMEM: return "out of memory";
 	case -ENODEV: return "no such HIP device";
 	case -EIO: return "HIP runtime error";
-	case -ENOENT: return "no demux tables loaded";
+	case -ENOENT: return "no demux tables / TX MAC table loaded";
 	default: return "unknown error";
 	}
 }
@@ -157,6 +167,11 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_defer);
 	hipFree(c->d_zero);
 	hipFree(c->d_present);
+	hipFree(c->d_dmacs);
+	hipFree(c->d_txbuf);
+	hipFree(c->d_txout);
+	hipFree(c->d_txsegs);
+	hipFree(c->d_txlen);
 	hipFree(c->d_frames);
 	hipFree(c->d_off);
 	hipFree(c->d_len);
@@ -621,6 +636,121 @@ int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, co
 	if (rc)
 		return rc;
 	HIPCHK(hipMemcpyAsync(out, c->d_dmx, n * sizeof(*out), hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	return 0;
+}
+
+/* ---- TX header build + checksums ----------------------- */
+
+int ixg_tx_set_macs(void *vctx, const uint8_t src_mac[6], const uint8_t *dmacs, uint32_t n_dmac)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !src_mac || (n_dmac && !dmacs))
+		return -EINVAL;
+	uint32_t *rows = (uint32_t *)calloc(n_dmac ? 2u * n_dmac : 2u, sizeof(uint32_t));
+	if (!rows)
+		return -ENOMEM;
+	for (uint32_t i = 0; i < n_dmac; i++)
+		memcpy(rows + 2u * i, dmacs + 6u * i, 6);
+	HIPCHK(hipSetDevice(c->device));
+	hipFree(c->d_dmacs);
+	c->d_dmacs = NULL;
+	c->n_dmac = 0;
+	if (hipMalloc((void **)&c->d_dmacs, (n_dmac ? n_dmac : 1u) * 8u) != hipSuccess ||
+	    hipMemcpy(c->d_dmacs, rows, (n_dmac ? n_dmac : 1u) * 8u, hipMemcpyHostToDevice) != hipSuccess) {
+		free(rows);
+		return -ENOMEM;
+	}
+	free(rows);
+	c->n_dmac = n_dmac;
+	memcpy(&c->smac_lo, src_mac, 4);
+	c->smac_hi = (uint32_t)src_mac[4] | ((uint32_t)src_mac[5] << 8);
+	return 0;
+}
+
+static int tx_launch(struct ixg_ctx *c, const void *seg_buf, const struct ixg_tx_seg *segs, uint32_t n, void *out,
+		     uint16_t *out_len, uint32_t flags, hipStream_t s)
+{
+	struct ixg_tparams p;
+	memset(&p, 0, sizeof(p));
+	p.seg_buf = (const uint8_t *)seg_buf;
+	p.segs = segs;
+	p.out = (uint8_t *)out;
+	p.out_len = out_len;
+	p.dmacs = c->d_dmacs;
+	p.n = n;
+	p.n_dmac = c->n_dmac;
+	p.smac_lo = c->smac_lo;
+	p.smac_hi = c->smac_hi;
+	p.flags = flags;
+	p.zero = c->d_zero;
+	return ixgrx_tx_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
+}
+
+int ixg_tx_batch_dev(void *vctx, const void *seg_buf, const struct ixg_tx_seg *segs, uint32_t n, void *out,
+		     uint16_t *out_len, uint32_t flags, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && (!seg_buf || !segs || !out || !out_len)) || (flags & ~IXG_TX_OFFLOAD))
+		return -EINVAL;
+	if (!c->d_dmacs)
+		return -ENOENT;
+	if (n == 0)
+		return 0;
+	return tx_launch(c, seg_buf, segs, n, out, out_len, flags, (hipStream_t)stream);
+}
+
+int ixg_tx_batch_host(void *vctx, const void *seg_buf, size_t seg_buf_len, const struct ixg_tx_seg *segs,
+		      uint32_t n, void *out, size_t out_size, uint16_t *out_len, uint32_t flags)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && (!seg_buf || !segs || !out || !out_len)) || (flags & ~IXG_TX_OFFLOAD))
+		return -EINVAL;
+	if (!c->d_dmacs)
+		return -ENOENT;
+	if (n == 0)
+		return 0;
+	/* frames must fit the output (the kernel writes whole 16-byte pieces) */
+	for (uint32_t i = 0; i < n; i++) {
+		uint64_t span = 34u + (uint64_t)segs[i].seg_len + (segs[i].proto == 17 ? 8u : 0u);
+		if (segs[i].out_off + ((span + 15u) & ~(uint64_t)15u) > out_size ||
+		    segs[i].seg_off + segs[i].seg_len > seg_buf_len)
+			return -EINVAL;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	if (seg_buf_len + IXG_TAIL_PAD > c->d_txbuf_cap) {
+		hipFree(c->d_txbuf);
+		c->d_txbuf = NULL;
+		c->d_txbuf_cap = 0;
+		HIPCHK(hipMalloc((void **)&c->d_txbuf, seg_buf_len + IXG_TAIL_PAD));
+		c->d_txbuf_cap = seg_buf_len + IXG_TAIL_PAD;
+	}
+	if (out_size > c->d_txout_cap) {
+		hipFree(c->d_txout);
+		c->d_txout = NULL;
+		c->d_txout_cap = 0;
+		HIPCHK(hipMalloc((void **)&c->d_txout, out_size));
+		c->d_txout_cap = out_size;
+	}
+	if (n > c->d_txn_cap) {
+		hipFree(c->d_txsegs);
+		hipFree(c->d_txlen);
+		c->d_txsegs = NULL;
+		c->d_txlen = NULL;
+		c->d_txn_cap = 0;
+		HIPCHK(hipMalloc((void **)&c->d_txsegs, (size_t)n * sizeof(struct ixg_tx_seg)));
+		HIPCHK(hipMalloc((void **)&c->d_txlen, (size_t)n * sizeof(uint16_t)));
+		c->d_txn_cap = n;
+	}
+	HIPCHK(hipMemcpyAsync(c->d_txbuf, seg_buf, seg_buf_len, hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemsetAsync(c->d_txbuf + seg_buf_len, 0, IXG_TAIL_PAD, c->stream));
+	HIPCHK(hipMemcpyAsync(c->d_txsegs, segs, (size_t)n * sizeof(*segs), hipMemcpyHostToDevice, c->stream));
+	HIPCHK(hipMemcpyAsync(c->d_txout, out, out_size, hipMemcpyHostToDevice, c->stream));
+	int rc = tx_launch(c, c->d_txbuf, c->d_txsegs, n, c->d_txout, c->d_txlen, flags, c->stream);
+	if (rc)
+		return rc;
+	HIPCHK(hipMemcpyAsync(out, c->d_txout, out_size, hipMemcpyDeviceToHost, c->stream));
+	HIPCHK(hipMemcpyAsync(out_len, c->d_txlen, (size_t)n * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipStreamSynchronize(c->stream));
 	return 0;
 }

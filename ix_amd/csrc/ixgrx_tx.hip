@@ -1,0 +1,262 @@
+// ixgrx_tx.hip - MI355X (gfx950) TX header build + checksums: the mirror of
+// the RX transform. For each struct ixg_tx_seg the frame
+// IX's TX paths build on the host -- the Ethernet header of ip_send_one
+// (dp/net/ip.c:198-213), the IPv4 header of tcp_output_packet
+// (dp/net/tcp_api.c:791-806) or of udp_output + ip_setup_header
+// (dp/net/udp.c:114-128, dp/net/net.h:65-78), the segment bytes -- plus the
+// checksums: the IP header's (chksum_internet, inc/asm/chksum.h:40-95) and
+// TCP's (the seed of inet_chksum_pseudo, dp/lwip/inet_chksum.c:324-357, for
+// a NIC that finishes it, or the full one the NIC would put on the wire).
+//
+// A wave takes 64 segments. Pass A, one lane per segment: descriptor, header
+// dwords, IP checksum and the TCP pseudo-header term, into per-wave LDS.
+// Pass B, G lanes per segment (G = 4 when every frame of the 64 is at most
+// 96 bytes, else 16): lane t of a group writes output piece k = j + 3 (16
+// bytes at frame + 16k) for body piece j = G*r + t - 1 of round r. The
+// headers are 34 (TCP) or 42 (UDP) bytes, so every output piece is bytes
+// 14..15 (TCP) or 6..15 (UDP) of body piece j followed by the start of piece
+// j + 1 (from the next lane by a shuffle, or loaded by the group's last
+// lane); "body piece -1" is the header's last 16 bytes. Loads are aligned
+// to the segment start (4-byte aligned), stores to the frame start (16-byte
+// aligned). TCP's body sum is reduced across the group and patched into
+// output piece 3 (frame bytes 48..63, the checksum at 50..51) last.
+//
+// No MFMA: HBM-bound byte moving (read the segment, write the frame).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ixgrx.h"
+#include "ixgrx_tx.h"
+
+#define DEV __device__ __forceinline__
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x2 u32x2_a4 __attribute__((aligned(4)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+using TParams = ixg_tparams;
+
+DEV uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+
+DEV uint32_t fold16(uint64_t s) {
+  s = (s & 0xffffffffull) + (s >> 32);
+  s = (s & 0xffffu) + (s >> 16);
+  s = (s & 0xffffu) + (s >> 16);
+  s = (s & 0xffffu) + (s >> 16);
+  return (uint32_t)s;
+}
+
+DEV uint32_t ones(int k) { return k >= 4 ? 0xffffffffu : (k <= 0 ? 0u : ((1u << (8 * k)) - 1u)); }
+
+// sum of the first `rem` bytes of a 16-byte piece as LE dwords (rest zero)
+DEV uint64_t piece_sum(const u32x4& v, int rem) {
+  return (uint64_t)(v.x & ones(rem)) + (v.y & ones(rem - 4)) + (v.z & ones(rem - 8)) + (v.w & ones(rem - 12));
+}
+
+// (a >> 16) | (b << 16): bytes 2..3 of a, then bytes 0..1 of b
+DEV uint32_t mid(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbyte(b, a, 2); }
+
+// per-wave pass-A results, one entry per segment of the chunk
+constexpr int kHdr = 11;  // frame bytes 0..43 as dwords
+struct WaveTx {
+  lds_u32* src_lo; lds_u32* src_hi; lds_u32* out_lo; lds_u32* out_hi;
+  lds_u32* meta;   // K (bits 0..15) | udp (16) | valid (17) | tcp_full (18)
+  lds_u32* seg_len;
+  lds_u32* l4term; // TCP: the seed (offload) or the pseudo-header sum (full)
+  lds_u32* hdr;    // [kHdr][64]
+};
+
+// Pass A: lane = segment. Returns the frame's piece count K (0 if invalid).
+DEV uint32_t tx_prepare(const TParams& p, uint32_t i, int lane, const WaveTx& w) {
+  const bool in = i < p.n;
+  const uint32_t* dp = reinterpret_cast<const uint32_t*>(p.segs + (in ? i : 0u));
+  const u32x4 a = *reinterpret_cast<const u32x4_a4*>(dp);
+  const u32x4 b = *reinterpret_cast<const u32x4_a4*>(dp + 4);
+  const u32x2 c = *reinterpret_cast<const u32x2_a4*>(dp + 8);
+  const uint64_t seg_off = a.x | ((uint64_t)a.y << 32), out_off = a.z | ((uint64_t)a.w << 32);
+  const uint32_t src = b.x, dst = b.y, seg_len = b.z & 0xffffu, sport = b.z >> 16;
+  const uint32_t dport = b.w & 0xffffu, proto = (b.w >> 16) & 0xffu, tos = b.w >> 24;
+  const uint32_t ttl = c.x & 0xffu, dmi = c.x >> 16;
+  const bool tcp = proto == 6u, udp = proto == 17u;
+  const uint32_t l4 = seg_len + (udp ? 8u : 0u);
+  const bool valid = in && (tcp || udp) && !(tcp && seg_len < 20u) && 20u + l4 <= 0xffffu && dmi < p.n_dmac &&
+                     (seg_off & 3u) == 0u && (out_off & 15u) == 0u;
+  const uint32_t flen = 34u + l4;
+  const u32x2 dm = *reinterpret_cast<const u32x2*>(p.dmacs + 2u * (valid ? dmi : 0u));
+  const bool offload = (p.flags & IXG_TX_OFFLOAD) != 0u;
+  // the header, dwords of frame bytes 0..43 (ip_send_one + tcp_output_packet
+  // / ip_setup_header + udp_output)
+  uint32_t h[kHdr];
+  h[0] = dm.x;
+  h[1] = (dm.y & 0xffffu) | (p.smac_lo << 16);
+  h[2] = (p.smac_lo >> 16) | (p.smac_hi << 16);
+  h[3] = 0x08u | (0x45u << 16) | ((tcp ? tos : 0u) << 24);      // type 0x0800, vhl, tos
+  h[4] = bswap16(20u + l4);                                      // len, id 0
+  h[5] = ((tcp ? ttl : 64u) << 16) | (proto << 24);              // off 0, ttl, proto
+  h[6] = (src & 0xffffu) << 16;                                  // chksum (below), src
+  h[7] = (src >> 16) | ((dst & 0xffffu) << 16);
+  h[8] = (dst >> 16) | (udp ? bswap16(sport) << 16 : 0u);
+  h[9] = udp ? (bswap16(dport) | (bswap16(l4) << 16)) : 0u;      // UDP len, checksum 0
+  h[10] = 0u;
+  // chksum_internet over bytes 14..33 (LE 16-bit words), unless a TCP frame
+  // leaves it to the NIC
+  if (udp || !offload) {
+    const uint64_t s = (uint64_t)(h[3] >> 16) + (h[4] & 0xffffu) + (h[4] >> 16) + (h[5] & 0xffffu) + (h[5] >> 16) +
+                       (h[6] >> 16) + (h[7] & 0xffffu) + (h[7] >> 16) + (dst >> 16);
+    h[6] |= (~fold16(s)) & 0xffffu;
+  }
+  uint32_t term = 0;
+  if (tcp && offload) {
+    // in_pseudo(src, dst, hton32(proto + tot_len)) (inet_chksum.c:324-340)
+    const uint64_t s = (uint64_t)src + dst + __builtin_bswap32(6u + seg_len);
+    uint32_t sum = (uint32_t)s + (uint32_t)(s >> 32);
+    sum = (sum & 0xffffu) + (sum >> 16);
+    term = sum > 0xffffu ? sum - 0xffffu : sum;
+  } else if (tcp) {
+    // pseudo header as inet_chksum_pseudo_partial adds it (:454-472, :436-437)
+    term = (src & 0xffffu) + (src >> 16) + (dst & 0xffffu) + (dst >> 16) + (6u << 8) + bswap16(seg_len);
+  }
+  const uint32_t K = valid ? (flen + 15u) >> 4 : 0u;
+  const uint64_t sa = reinterpret_cast<uint64_t>(p.seg_buf) + seg_off;
+  const uint64_t oa = reinterpret_cast<uint64_t>(p.out) + out_off;
+  w.src_lo[lane] = (uint32_t)sa;
+  w.src_hi[lane] = (uint32_t)(sa >> 32);
+  w.out_lo[lane] = (uint32_t)oa;
+  w.out_hi[lane] = (uint32_t)(oa >> 32);
+  w.meta[lane] = K | (udp ? 1u << 16 : 0u) | (valid ? 1u << 17 : 0u) | (tcp && !offload ? 1u << 18 : 0u);
+  w.seg_len[lane] = seg_len;
+  w.l4term[lane] = term;
+#pragma unroll
+  for (int k = 0; k < kHdr; k++) w.hdr[k * 64 + lane] = h[k];
+  if (in) p.out_len[i] = (uint16_t)(valid ? flen : 0u);
+  return K;
+}
+
+DEV void store16(uint64_t addr, const u32x4& v) { *reinterpret_cast<u32x4*>(addr) = v; }
+
+// Pass B: G lanes per segment, 64 / G segments at a time.
+template <int G>
+DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
+  const int g = lane / G, t = lane % G;
+  for (int s0 = 0; s0 < 64; s0 += 64 / G) {
+    const int si = s0 + g;
+    const uint32_t meta = w.meta[si];
+    const bool valid = (meta >> 17) & 1u, udp = (meta >> 16) & 1u, full = (meta >> 18) & 1u;
+    const int K = (int)(meta & 0xffffu);
+    const int seg_len = (int)w.seg_len[si];
+    const uint64_t src = ((uint64_t)w.src_hi[si] << 32) | w.src_lo[si];
+    const uint64_t out = ((uint64_t)w.out_hi[si] << 32) | w.out_lo[si];
+    // header dwords this lane may need
+    const int hb = udp ? 6 : 4;  // body piece -1 = frame bytes [H - 16, H): dwords hb..hb+4
+    uint32_t hp[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) hp[k] = w.hdr[(hb + k) * 64 + si];
+    const u32x4 pm1 = {mid(hp[0], hp[1]), mid(hp[1], hp[2]), mid(hp[2], hp[3]), mid(hp[3], hp[4])};
+    const int nr = valid ? (K - 2 + G - 1) / G : 0;  // output pieces 2..K-1
+    uint64_t acc = 0;
+    u32x4 held = {0u, 0u, 0u, 0u};
+    for (int r = 0; __any(r < nr); r++) {
+      const bool act = r < nr;
+      const int j = G * r + t - 1;
+      // always-issued loads (the zero page when there is nothing to read)
+      const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
+      const bool lo = act && j >= 0, ln = act && t == G - 1;
+      const u32x4 v = *reinterpret_cast<const u32x4_a4*>(lo ? src + 16u * (uint32_t)j : zero);
+      const u32x4 vn = *reinterpret_cast<const u32x4_a4*>(ln ? src + 16u * (uint32_t)(j + 1) : zero);
+      const u32x4 own = j < 0 ? pm1 : v;
+      u32x4 nxt;
+      nxt.x = (uint32_t)__shfl_down((int)own.x, 1, G);
+      nxt.y = (uint32_t)__shfl_down((int)own.y, 1, G);
+      nxt.z = (uint32_t)__shfl_down((int)own.z, 1, G);
+      nxt.w = (uint32_t)__shfl_down((int)own.w, 1, G);
+      if (t == G - 1) nxt = vn;
+      // output piece k = j + 3: bytes 14..15 (TCP) / 6..15 (UDP) of own,
+      // then the start of nxt
+      u32x4 o;
+      if (udp) {
+        o = {mid(own.y, own.z), mid(own.z, own.w), mid(own.w, nxt.x), mid(nxt.x, nxt.y)};
+      } else {
+        o = {mid(own.w, nxt.x), mid(nxt.x, nxt.y), mid(nxt.y, nxt.z), mid(nxt.z, nxt.w)};
+      }
+      const int k = j + 3;
+      if (act && k < K) {
+        if (!udp && k == 3)
+          held = o;  // holds the TCP checksum: stored after the reduction
+        else
+          store16(out + 16u * (uint32_t)k, o);
+      }
+      if (act && r == 0 && t == 0) {
+        store16(out, u32x4{w.hdr[0 * 64 + si], w.hdr[1 * 64 + si], w.hdr[2 * 64 + si], w.hdr[3 * 64 + si]});
+        store16(out + 16u, u32x4{w.hdr[4 * 64 + si], w.hdr[5 * 64 + si], w.hdr[6 * 64 + si], w.hdr[7 * 64 + si]});
+      }
+      // body piece j + 1 is summed by the lane it is `nxt` for: pieces
+      // 0..K-3 are, which covers the segment (K - 2 >= ceil(seg_len / 16))
+      if (full && act) {
+        u32x4 sv = nxt;
+        if (j == 0) sv.x &= 0xffff0000u;  // the checksum field (segment bytes 16..17) counts as 0
+        acc += piece_sum(sv, seg_len - 16 * (j + 1));
+      }
+    }
+    if (!udp) {
+#pragma unroll
+      for (int m = 1; m < G; m <<= 1) {
+        const uint32_t lo32 = (uint32_t)__shfl_xor((int)(uint32_t)acc, m, G);
+        const uint32_t hi32 = (uint32_t)__shfl_xor((int)(uint32_t)(acc >> 32), m, G);
+        acc += ((uint64_t)hi32 << 32) | lo32;
+      }
+      if (valid && t == 1) {
+        const uint32_t term = w.l4term[si];
+        const uint32_t ck = full ? (~fold16(acc + term)) & 0xffffu : term;
+        held.x = (held.x & 0xffffu) | (ck << 16);
+        store16(out + 48u, held);
+      }
+    }
+  }
+}
+
+DEV void tx_loop(const TParams& p, const WaveTx& w) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * kWaves;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < nchunks; c += nw) {
+    const uint32_t K = tx_prepare(p, c * 64u + (uint32_t)lane, lane, w);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (__all(K <= 6u))
+      tx_stream<4>(p, lane, w);
+    else
+      tx_stream<16>(p, lane, w);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_tx_build(TParams p) {
+  __shared__ uint32_t sh[kWaves][(7 + kHdr) * 64];
+  lds_u32* b = (lds_u32*)sh[threadIdx.x >> 6];
+  const WaveTx w{b, b + 64, b + 128, b + 192, b + 256, b + 320, b + 384, b + 448};
+  tx_loop(p, w);
+}
+
+extern "C" int ixgrx_tx_launch(const void* params, uint32_t ncu, void* stream) {
+  const TParams& p = *static_cast<const TParams*>(params);
+  const uint64_t nchunks = ((uint64_t)p.n + 63u) / 64u;
+  const uint64_t want = (nchunks + kWaves - 1) / kWaves;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ixg_tx_build, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
+  const uint64_t cap = (uint64_t)ncu * (uint64_t)nb;
+  const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+  hipLaunchKernelGGL(ixg_tx_build, dim3(grid ? grid : 1u), dim3(kBlock), 0, (hipStream_t)stream, p);
+  return (int)hipGetLastError();
+}

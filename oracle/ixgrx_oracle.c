@@ -698,3 +698,111 @@ int ixgo_demux_batch(const struct ixg_demux_tables *t, uint32_t fg_base, const u
 	}
 	return 0;
 }
+
+/* ---- TX: header build + checksums ------------------------ */
+
+/*
+ * in_pseudo + inet_chksum_pseudo (dp/lwip/inet_chksum.c:324-357): the seed
+ * lwIP leaves in the TCP checksum field for the NIC:
+ * in_pseudo(src, dst, hton32(proto + tot_len)) -- a 32-bit add/adc/adc $0
+ * chain, one 16-bit fold, and a conditional subtract of 0xffff.
+ */
+uint16_t ixgo_pseudo_seed(uint32_t src_raw, uint32_t dst_raw, uint8_t proto, uint16_t tot_len)
+{
+	uint32_t c = __builtin_bswap32((uint32_t)proto + tot_len);
+	uint64_t s = (uint64_t)src_raw + dst_raw + c; /* addl; adcl; adcl $0 */
+	uint32_t sum = (uint32_t)s + (uint32_t)(s >> 32);
+	sum = (sum & 0xffff) + (sum >> 16);
+	if (sum > 0xffff)
+		sum -= 0xffff;
+	return (uint16_t)sum;
+}
+
+static void put16be(uint8_t *p, uint16_t v)
+{
+	p[0] = (uint8_t)(v >> 8);
+	p[1] = (uint8_t)v;
+}
+
+/*
+ * One TX frame (include/ixgrx.h struct ixg_tx_seg). Returns the frame length,
+ * 0 for an invalid segment (proto not 6/17, a TCP segment shorter than its
+ * 20-byte header, a datagram longer than 65535 bytes).
+ *  - Ethernet: ip_send_one (dp/net/ip.c:198-213): dhost = dmac, shost =
+ *    src_mac, type 0x0800.
+ *  - TCP, tcp_output_packet (dp/net/tcp_api.c:791-812): vhl 0x45, tos/ttl
+ *    from the pcb, len 20 + seg_len, id 0, off 0, proto 6, checksum 0,
+ *    src/dst raw; the segment copied after it. The TCP checksum field
+ *    (segment bytes 16..17) holds lwIP's seed inet_chksum_pseudo
+ *    (inet_chksum.c:353-357). IXG_TX_OFFLOAD stops there (what the NIC is
+ *    handed, tcp_api.c:815-817); otherwise [NIC] the IP checksum is
+ *    chksum_internet of the header and the TCP checksum is the one's
+ *    complement of the sum over the pseudo header and the segment, i.e.
+ *    lwIP's inet_chksum_pseudo_partial with chksum_len = seg_len over the
+ *    segment with the field zeroed.
+ *  - UDP, udp_output (dp/net/udp.c:114-128) with ip_setup_header
+ *    (dp/net/net.h:65-78): tos 0, ttl 64, proto 17, len 28 + seg_len, IP
+ *    checksum by chksum_internet in software, UDP header {sport, dport,
+ *    len 8 + seg_len, checksum 0}, then the payload.
+ */
+uint32_t ixgo_tx_one(const uint8_t *seg, const struct ixg_tx_seg *d, const uint8_t src_mac[6],
+		     const uint8_t dmac[6], uint32_t flags, uint8_t *out)
+{
+	const int tcp = d->proto == 6, udp = d->proto == 17;
+	const uint32_t l4 = (uint32_t)d->seg_len + (udp ? 8u : 0u);
+	if ((!tcp && !udp) || (tcp && d->seg_len < 20) || 20u + l4 > 0xffffu)
+		return 0;
+	memcpy(out, dmac, 6);
+	memcpy(out + 6, src_mac, 6);
+	out[12] = 0x08;
+	out[13] = 0x00;
+	uint8_t *ip = out + 14;
+	ip[0] = 0x45;
+	ip[1] = tcp ? d->tos : 0;
+	put16be(ip + 2, (uint16_t)(20u + l4));
+	put16be(ip + 4, 0);
+	put16be(ip + 6, 0);
+	ip[8] = tcp ? d->ttl : 64;
+	ip[9] = d->proto;
+	ip[10] = ip[11] = 0;
+	memcpy(ip + 12, &d->src_ip, 4);
+	memcpy(ip + 16, &d->dst_ip, 4);
+	uint8_t *l4p = ip + 20;
+	if (udp) {
+		put16be(l4p, d->src_port);
+		put16be(l4p + 2, d->dst_port);
+		put16be(l4p + 4, (uint16_t)l4);
+		l4p[6] = l4p[7] = 0;
+		memcpy(l4p + 8, seg, d->seg_len);
+		uint16_t c = ixgo_chksum_internet(ip, 20);
+		memcpy(ip + 10, &c, 2);
+		return 14u + 20u + l4;
+	}
+	memcpy(l4p, seg, d->seg_len);
+	if (flags & IXG_TX_OFFLOAD) {
+		uint16_t s = ixgo_pseudo_seed(d->src_ip, d->dst_ip, 6, d->seg_len);
+		memcpy(l4p + 16, &s, 2);
+	} else {
+		l4p[16] = l4p[17] = 0;
+		uint16_t c = ixgo_pseudo_partial(l4p, d->seg_len, 6, d->seg_len, d->src_ip, d->dst_ip);
+		memcpy(l4p + 16, &c, 2);
+		uint16_t ic = ixgo_chksum_internet(ip, 20);
+		memcpy(ip + 10, &ic, 2);
+	}
+	return 14u + 20u + l4;
+}
+
+int ixgo_tx_batch(const uint8_t *seg_buf, const struct ixg_tx_seg *segs, uint32_t n, const uint8_t src_mac[6],
+		  const uint8_t *dmacs, uint32_t n_dmac, uint32_t flags, uint8_t *out, uint16_t *out_len)
+{
+	for (uint32_t i = 0; i < n; i++) {
+		const struct ixg_tx_seg *d = &segs[i];
+		if (d->dmac_idx >= n_dmac || (d->seg_off & 3) || (d->out_off & 15)) {
+			out_len[i] = 0;
+			continue;
+		}
+		out_len[i] = (uint16_t)ixgo_tx_one(seg_buf + d->seg_off, d, src_mac, dmacs + 6u * d->dmac_idx, flags,
+						   out + d->out_off);
+	}
+	return 0;
+}

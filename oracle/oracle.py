@@ -51,6 +51,10 @@ def lib() -> ctypes.CDLL:
         L.ixgo_tcp_to_idx.restype = u16
         L.ixgo_pseudo_partial.argtypes = [vp, u16, u8, u16, u32, u32]
         L.ixgo_pseudo_partial.restype = u16
+        L.ixgo_pseudo_seed.argtypes = [u32, u32, u8, u16]
+        L.ixgo_pseudo_seed.restype = u16
+        L.ixgo_tx_batch.argtypes = [vp, vp, u32, vp, vp, u32, u32, vp, vp]
+        L.ixgo_tx_batch.restype = i32
         _lib = L
     return _lib
 
@@ -161,3 +165,21 @@ def demux_batch(nfg: int, active_start, active, tw_start, tw, listen, fg_base: i
     L.ixgo_demux_batch(ctypes.byref(t), fg_base, blob.ctypes.data, None if offa is None else offa.ctypes.data,
                        lens.ctypes.data, stride, n, rec.ctypes.data, out.ctypes.data)
     return out
+
+
+def tx_batch(seg_buf: np.ndarray, segs: np.ndarray, src_mac: bytes, dmacs: np.ndarray, out_size: int,
+             flags: int = 0):
+    """TX frames for struct ixg_tx_seg rows `segs` (oracle/ixgrx_oracle.c
+    ixgo_tx_batch). Returns (output buffer, frame lengths)."""
+    L = lib()
+    buf = np.ascontiguousarray(seg_buf, dtype=np.uint8)
+    sg = np.ascontiguousarray(segs)
+    assert sg.dtype.itemsize == 40
+    d = np.ascontiguousarray(dmacs, dtype=np.uint8).reshape(-1, 6)
+    src = np.frombuffer(bytes(src_mac), dtype=np.uint8).copy()
+    n = int(sg.shape[0])
+    out = np.zeros(out_size, dtype=np.uint8)
+    out_len = np.zeros(n, dtype=np.uint16)
+    L.ixgo_tx_batch(buf.ctypes.data, sg.ctypes.data, n, src.ctypes.data, d.ctypes.data, d.shape[0], flags,
+                    out.ctypes.data, out_len.ctypes.data)
+    return out, out_len

@@ -34,4 +34,12 @@ struct ref_pcb {
 };
 int ref_find_list(const struct ref_pcb *pcbs, int n, uint32_t src_raw, uint32_t dst_raw, uint16_t src_port,
 		  uint16_t dst_port);
+
+/* TX: reference frame builds and the offload seed */
+void ref_tx_set_macs(const uint8_t src[6], const uint8_t dst[6]);
+uint32_t ref_tcp_frame(uint32_t local_raw, uint32_t remote_raw, uint8_t tos, uint8_t ttl, const void *seg,
+		       uint16_t len, uint8_t *out);
+uint32_t ref_udp_frame(uint32_t src_raw, uint32_t dst_raw, uint16_t sport, uint16_t dport, const void *payload,
+		       uint16_t len, uint8_t *out);
+uint16_t ref_pseudo_seed(uint32_t src_raw, uint32_t dst_raw, uint8_t proto, uint16_t tot_len);
 #endif

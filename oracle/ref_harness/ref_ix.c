@@ -111,3 +111,80 @@ uint16_t ref_chksum_internet(const void *buf, int len)
 {
 	return chksum_internet((const char *)buf, len);
 }
+
+/* ---- TX test doubles (the reference's TX path) ---- */
+/* mempool slow path (mbuf_alloc_local -> mempool_alloc_2 when the per-CPU
+ * free list is empty, as it always is here): one zeroed IX mbuf element */
+static uint8_t tx_mbuf[2112] __attribute__((aligned(64)));
+void *mempool_alloc_2(struct mempool *m)
+{
+	(void)m;
+	memset(tx_mbuf, 0, sizeof(tx_mbuf));
+	return tx_mbuf;
+}
+void mbuf_default_done(struct mbuf *m) { (void)m; }
+
+/* the ARP table row ip_send_one finds (dp/net/ip.c:208) */
+static struct eth_addr arp_mac;
+int arp_lookup_mac(struct ip_addr *addr, struct eth_addr *mac)
+{
+	(void)addr;
+	*mac = arp_mac;
+	return 0;
+}
+int arp_add_pending_pkt(struct ip_addr *dst_addr, struct eth_fg *fg, struct mbuf *mbuf, size_t len)
+{
+	(void)dst_addr;
+	(void)fg;
+	(void)mbuf;
+	(void)len;
+	return -1;
+}
+
+void ref_tx_set_macs(const uint8_t src[6], const uint8_t dst[6])
+{
+	memcpy(&CFG.mac, src, 6);
+	memcpy(&arp_mac, dst, 6);
+}
+
+void *ref_cur_fg(void) { return &the_fg; }
+
+/* The frame the last eth_send_one queued (its mbuf data and mbuf->len);
+ * returns the length, 0 when nothing was queued. */
+uint32_t ref_tx_take(uint8_t *out)
+{
+	if (!the_txq.len)
+		return 0;
+	struct mbuf *m = the_txq.bufs[the_txq.len - 1];
+	the_txq.len = 0;
+	the_txq.cap = 1 << 30;
+	memcpy(out, mbuf_mtod(m, uint8_t *), m->len);
+	return (uint32_t)m->len;
+}
+
+/* [UDP] udp_output (dp/net/udp.c:114-128) is unbuildable here (udp.c needs
+ * Dune's mmu-x86.h); its header writes are restated over the reference's own
+ * ip_setup_header (dp/net/net.h:65-78) and chksum_internet, and the frame is
+ * queued through the reference's ip_send_one's Ethernet fill-in instead of
+ * udp_output's inline copy of it (udp.c:115-117, the same three writes). */
+uint32_t ref_udp_frame(uint32_t src_raw, uint32_t dst_raw, uint16_t sport, uint16_t dport, const void *payload,
+		       uint16_t len, uint8_t *out)
+{
+	struct mbuf *pkt = mbuf_alloc_local();
+	struct eth_hdr *ethhdr = mbuf_mtod(pkt, struct eth_hdr *);
+	struct ip_hdr *iphdr = mbuf_nextd(ethhdr, struct ip_hdr *);
+	struct udp_hdr *udphdr = mbuf_nextd(iphdr, struct udp_hdr *);
+	size_t full_len = len + sizeof(struct udp_hdr);
+	struct ip_addr dst;
+	ip_setup_header(iphdr, IPPROTO_UDP, ntoh32(src_raw), ntoh32(dst_raw), full_len);
+	iphdr->chksum = chksum_internet((void *)iphdr, sizeof(struct ip_hdr));
+	udphdr->src_port = hton16(sport);
+	udphdr->dst_port = hton16(dport);
+	udphdr->len = hton16(full_len);
+	udphdr->chksum = 0;
+	memcpy(udphdr + 1, payload, len);
+	dst.addr = ntoh32(dst_raw);
+	if (ip_send_one(&the_fg, &dst, pkt, sizeof(struct eth_hdr) + sizeof(struct ip_hdr) + full_len))
+		return 0;
+	return ref_tx_take(out);
+}

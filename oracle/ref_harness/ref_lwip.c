@@ -52,3 +52,15 @@ int ref_tcp_to_idx(uint32_t local_raw, uint32_t remote_raw, uint16_t local_port,
 }
 
 /* pbuf.c's unreachable allocators reference these; never called here */
+
+/* inet_chksum_pseudo (inet_chksum.c:353-357): the TX offload seed */
+uint16_t ref_pseudo_seed(uint32_t src_raw, uint32_t dst_raw, uint8_t proto, uint16_t tot_len)
+{
+	struct pbuf p;
+	ip_addr_t s, d;
+	memset(&p, 0, sizeof(p));
+	p.tot_len = tot_len;
+	s.addr = src_raw;
+	d.addr = dst_raw;
+	return inet_chksum_pseudo(&p, proto, tot_len, &s, &d);
+}

@@ -91,3 +91,20 @@ def test_dispatch_host_only():
     got = lib.ixg_rx_dispatch(mb.ctypes.data, recs.ctypes.data, 6, ctypes.cast(ctypes.pointer(ops), ctypes.c_void_p), None)
     assert got == 4
     assert seen == [("tcp", 100), ("udp", 101), ("icmp", 102), ("arp", 103), ("drop", 104), ("drop", 105)]
+
+
+def test_tx_seg_layout_matches_header():
+    """struct ixg_tx_seg as the C compiler lays it out (offsetof via gcc)."""
+    import subprocess
+    import tempfile
+    from ix_amd import tx
+    fields = [n for n in tx.SEG_DTYPE.names]
+    src = "#include <stdio.h>\n#include <stddef.h>\n#include \"ixgrx.h\"\nint main(void){printf(\"%zu\", sizeof(struct ixg_tx_seg));"
+    src += "".join(f'printf(" %zu", offsetof(struct ixg_tx_seg, {f}));' for f in fields) + "return 0;}"
+    with tempfile.TemporaryDirectory() as td:
+        c, exe = os.path.join(td, "t.c"), os.path.join(td, "t")
+        open(c, "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), c, "-o", exe], check=True)
+        got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+    assert got[0] == tx.SEG_DTYPE.itemsize
+    assert got[1:] == [tx.SEG_DTYPE.fields[f][1] for f in fields]
