@@ -216,6 +216,13 @@ def parity_leg(checks, key) -> dict:
             _, name, pool, flags, rec, tiled = c
             er, _ = oracle.rx_trace(pool, key, flags=flags, threads=8, hash_mode=oracle.HASH_TABLE)
             res[name] = "ok" if tiled and np.array_equal(rec, er) else "MISMATCH"
+        elif c[0] == "tx":
+            _, kind, (buf, segs, smac, dmacs, out, out_len), tiled = c
+            size = int(segs["out_off"][-1]) + 2048
+            eo, el = oracle.tx_batch(buf, segs, smac, dmacs, size, 0)
+            ok = np.array_equal(el, out_len) and all(
+                np.array_equal(out[o:o + L], eo[o:o + L]) for o, L in zip(segs["out_off"].astype(np.int64), el))
+            res["tx_" + kind] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
         else:
             _, pool, tabs, rec, dmx, tiled = c
             er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
@@ -309,6 +316,53 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
             "parity": "pending"}, check
 
 
+def tx_line(dev, steps: int, eng, kind: str, n: int):
+    """TX header build + checksums: n segments tiled from 2^16
+    distinct ones, frames packed 16-byte aligned in HBM; a step = one
+    ixg_tx_batch_dev launch (full checksums, as the NIC puts them on the
+    wire)."""
+    import torch
+    from ix_amd import tx
+    b = tx.make_segments(kind, n, seed=0x1BE000 + n, pool=1 << 16, layout="packed")
+    tx.set_macs(eng, b.src_mac, b.dmacs)
+    buf = torch.from_numpy(b.buf).to(dev)
+    segs = torch.from_numpy(b.segs.view(np.uint8)).to(dev)
+    out = torch.empty(b.out_size, dtype=torch.uint8, device=dev)
+    out_len = torch.empty(n, dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def launch():
+        tx.batch_dev(eng, buf.data_ptr(), segs.data_ptr(), n, out.data_ptr(), out_len.data_ptr(), 0,
+                     stream.cuda_stream)
+    for _ in range(3):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, c in ev:
+        a.record(stream)
+        launch()
+        c.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = float(np.mean([a.elapsed_time(c) * 1e-3 for a, c in ev]))
+    pool = 1 << 16
+    reps = n // pool
+    span = int(b.segs["out_off"][pool]) if reps > 1 else b.out_size
+    rows = out[:reps * span].view(reps, span)
+    tiled = bool(torch.equal(rows, rows[:1].expand(reps, -1)))
+    L = b.segs["seg_len"].astype(np.float64)
+    flen = 34 + L + np.where(b.segs["proto"] == 17, 8, 0)
+    alg = float((40 + L + flen + 2).mean())  # descriptor + segment read, frame + length written
+    first = (b.buf[:int(b.segs["seg_off"][pool]) if reps > 1 else b.buf.size + 0], b.segs[:pool].copy(),
+             b.src_mac, b.dmacs, out[:span].cpu().numpy(), out_len[:pool].cpu().numpy().astype(np.uint16))
+    return {"workload": f"TX build over {n} {kind} segments (frames packed in HBM, full checksums; "
+                        "kernel ixg_tx_build)",
+            "mpps": round(n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
+            "alg_bytes_per_pkt": round(alg, 1), "roofline_frac": round(alg * n / k / 1e9 / PEAK_HBM_GBPS, 4),
+            "parity": "tiled-consistent" if tiled else "MISMATCH"}, ("tx", kind, first, tiled)
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -332,6 +386,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy", action="store_true")
     ap.add_argument("--no-demux", action="store_true")
+    ap.add_argument("--no-tx", action="store_true")
     ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
     args = ap.parse_args()
 
@@ -412,6 +467,13 @@ def main():
         res["demux"], dchk = demux_line(dev, key, max(5, args.steps // 2), rank, engine)
         checks.append(dchk)
         wl = None
+    if not args.no_tx and args.workload == "c2":
+        torch.cuda.empty_cache()
+        res["tx"] = {}
+        for kind, n in (("tcp64", 16 * 1024 * 1024), ("tcp1514", 4 * 1024 * 1024)):
+            res["tx"][kind], tchk = tx_line(dev, max(5, args.steps // 2), engine(0), kind, n)
+            checks.append(tchk)
+            torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_copy:
         del wl
         torch.cuda.empty_cache()
@@ -430,6 +492,8 @@ def main():
         if "demux" in res:
             res["demux"]["parity"] = par["demux"]
             res["demux"]["kinds"] = par["demux_kinds"]
+        for kind in res.get("tx", {}):
+            res["tx"][kind]["parity"] = par["tx_" + kind]
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

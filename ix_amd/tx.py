@@ -151,7 +151,10 @@ def make_segments(kind: str, n: int, seed: int, pool: int | None = None, layout:
     if m < n:
         reps = n // m
         assert n % m == 0
-        buf = np.concatenate([np.tile(buf[:total], reps), buf[total:]])
+        # the tail repeats the pool's first bytes, so the bytes past each
+        # repetition's last segment (read as padding) are the same in every
+        # repetition
+        buf = np.concatenate([np.tile(buf[:total], reps), buf[:64]])
         seg_off = (seg_off[None, :] + total * np.arange(reps)[:, None]).reshape(-1)
         proto, seg_len = np.tile(proto, reps), np.tile(seg_len, reps)
     segs = np.zeros(n, dtype=SEG_DTYPE)
