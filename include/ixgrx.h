@@ -333,6 +333,51 @@ int ixg_tx_batch_dev(void *ctx, const void *seg_buf, const struct ixg_tx_seg *se
 int ixg_tx_batch_host(void *ctx, const void *seg_buf, size_t seg_buf_len, const struct ixg_tx_seg *segs,
 		      uint32_t n, void *out, size_t out_size, uint16_t *out_len, uint32_t flags);
 
+/* ---- event records: the usys descriptors libix consumes ---- */
+
+/* struct bsys_desc (inc/ix/syscall.h:101-104), 40 bytes packed */
+struct ixg_bsys_desc {
+	uint64_t sysnr;
+	uint64_t arga, argb, argc, argd;
+};
+#define IXG_USYS_UDP_RECV 0u /* inc/ix/syscall.h:319 */
+#define IXG_USYS_TCP_RECV 4u /* :323 */
+
+/* What recv_a_pbuf needs of a PCB (dp/net/tcp_api.c:125-147): its index in
+ * the pcb mempool (the low 48 bits of the flow handle, tcpapi_to_handle
+ * :125-131) and the application's cookie. Indexed by ixg_pcb_key.id. */
+struct ixg_ev_pcb {
+	uint64_t pcb_idx;
+	uint64_t cookie;
+};
+
+/* flags of ixg_ev_batch_dev */
+#define IXG_EV_UDP_TUPLE (1u << 0) /* also write udp_input's struct ip_tuple
+                                      (host-order src/dst IP and ports) over the
+                                      first 12 bytes of each UDP frame, as
+                                      dp/net/udp.c:81-86 does */
+
+/* Emit, in frame order, the descriptors the reference's stack writes into the
+ * per-CPU usys array for a batch (dense, as usys_next hands them out):
+ *  - IXG_V_UDP: udp_input's usys_udp_recv (udp.c:88, syscall.h:360-365):
+ *    {USYS_UDP_RECV, iomap(payload), udp->len, iomap(frame start: the
+ *    ip_tuple), 0};
+ *  - IXG_V_TCP whose demux record is IXG_D_ACTIVE with a non-empty payload:
+ *    recv_a_pbuf's usys_tcp_recv (tcp_api.c:133-147, syscall.h:416-420) for
+ *    the segment delivered in order as one pbuf: {USYS_TCP_RECV,
+ *    (fg_id << 48) | pcb_idx, cookie, iomap(payload), payload length}. The
+ *    TCP state machine (tcp_process) that decides in-order delivery stays on
+ *    the host: these are the descriptors for in-order segments.
+ * iomap(frame i + x) = iomap_base + frame offset of i + x (frames laid out as
+ * the device batch: a mirror of the mbuf arena gives IX's
+ * mempool_pagemem_to_iomap, inc/ix/mempool.h:259-263). d_dmx may be NULL (no
+ * TCP events); d_frame_idx (may be NULL) receives each event's frame index.
+ * *d_count (device u32) receives the number of events. Asynchronous. */
+int ixg_ev_batch_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec,
+		     const struct ixg_demux_rec *d_dmx, const struct ixg_ev_pcb *d_pcbs, uint32_t n_pcbs,
+		     uint32_t n, uint64_t iomap_base, uint32_t flags, struct ixg_bsys_desc *d_ev,
+		     uint32_t *d_frame_idx, uint32_t *d_count, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -16,6 +16,7 @@
 #include "ixgrx_internal.h"
 #include "ixgrx_demux.h"
 #include "ixgrx_tx.h"
+#include "ixgrx_ev.h"
 
 struct ixg_ctx {
 	int device;
@@ -63,6 +64,9 @@ struct ixg_ctx {
 	struct ixg_tx_seg *d_txsegs;
 	uint16_t *d_txlen;
 	size_t d_txn_cap;
+	/* event emission scratch: per-chunk counts / bases */
+	uint32_t *d_evbase;
+	size_t evbase_cap;
 };
 
 /* ---- hash tables -------------------------------------------------------- */
@@ -172,6 +176,7 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_txout);
 	hipFree(c->d_txsegs);
 	hipFree(c->d_txlen);
+	hipFree(c->d_evbase);
 	hipFree(c->d_frames);
 	hipFree(c->d_off);
 	hipFree(c->d_len);
@@ -753,4 +758,45 @@ int ixg_tx_batch_host(void *vctx, const void *seg_buf, size_t seg_buf_len, const
 	HIPCHK(hipMemcpyAsync(out_len, c->d_txlen, (size_t)n * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
 	HIPCHK(hipStreamSynchronize(c->stream));
 	return 0;
+}
+
+/* ---- event records --------------------------------------- */
+
+int ixg_ev_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec,
+		     const struct ixg_demux_rec *d_dmx, const struct ixg_ev_pcb *d_pcbs, uint32_t n_pcbs,
+		     uint32_t n, uint64_t iomap_base, uint32_t flags, struct ixg_bsys_desc *d_ev,
+		     uint32_t *d_frame_idx, uint32_t *d_count, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || !d_count || (flags & ~IXG_EV_UDP_TUPLE))
+		return -EINVAL;
+	if (n && (!fr->base || !d_rec || !d_ev || (d_dmx && n_pcbs && !d_pcbs) || (!fr->off && (fr->stride & 3))))
+		return -EINVAL;
+	if (n == 0)
+		return hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream) == hipSuccess ? 0 : -EIO;
+	size_t nchunks = ((size_t)n + 63) / 64;
+	if (nchunks > c->evbase_cap) {
+		hipFree(c->d_evbase);
+		c->d_evbase = NULL;
+		c->evbase_cap = 0;
+		HIPCHK(hipMalloc((void **)&c->d_evbase, nchunks * sizeof(uint32_t)));
+		c->evbase_cap = nchunks;
+	}
+	struct ixg_eparams p;
+	memset(&p, 0, sizeof(p));
+	p.base = (uint8_t *)fr->base;
+	p.off = fr->off;
+	p.rec = d_rec;
+	p.dmx = d_dmx;
+	p.pcbs = d_pcbs;
+	p.ev = d_ev;
+	p.frame_idx = d_frame_idx;
+	p.count = d_count;
+	p.chunk_base = c->d_evbase;
+	p.iomap_base = iomap_base;
+	p.stride = fr->stride;
+	p.n = n;
+	p.n_pcbs = d_dmx ? n_pcbs : 0;
+	p.flags = flags;
+	return ixgrx_ev_launch(&p, c->ncu, stream) == 0 ? 0 : -EIO;
 }

@@ -48,6 +48,7 @@ EXPORTS = (
     "ixg_rx_hash_tables", "ixg_abi_version", "ixg_strerror", "ixg_rx_dispatch",
     "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host",
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
+    "ixg_ev_batch_dev",
 )
 
 

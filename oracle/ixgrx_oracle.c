@@ -806,3 +806,64 @@ int ixgo_tx_batch(const uint8_t *seg_buf, const struct ixg_tx_seg *segs, uint32_
 	}
 	return 0;
 }
+
+/* ---- event records ---------------------------------------- */
+
+/*
+ * The usys descriptors of a batch, dense and in frame order (include/ixgrx.h
+ * ixg_ev_batch_dev):
+ *  - udp_input (dp/net/udp.c:81-88): the ip_tuple written over the frame
+ *    start (IXG_EV_UDP_TUPLE), then usys_udp_recv(iomap(data), udp->len,
+ *    iomap(id)) = BSYS_DESC_3ARG (inc/ix/syscall.h:121-123,360-365);
+ *  - recv_a_pbuf (dp/net/tcp_api.c:133-147) for a segment delivered in order
+ *    as one pbuf: usys_tcp_recv(handle, cookie, iomap(payload), len) =
+ *    BSYS_DESC_4ARG (:124-126,416-420), handle = tcpapi_to_handle
+ *    (:125-131): pcb mempool index | fg_id << 48.
+ * iomap(p) = p + iomap_offset (inc/ix/mempool.h:259-263), here
+ * iomap_base + frame offset + x. Returns the number of descriptors.
+ */
+uint32_t ixgo_ev_batch(uint8_t *base, const uint64_t *off, uint32_t stride, const struct ixg_rx_rec *rec,
+		       const struct ixg_demux_rec *dmx, const struct ixg_ev_pcb *pcbs, uint32_t n_pcbs, uint32_t n,
+		       uint64_t iomap_base, uint32_t flags, struct ixg_bsys_desc *ev, uint32_t *frame_idx)
+{
+	uint32_t k = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		const struct ixg_rx_rec *r = &rec[i];
+		const uint64_t o = off ? off[i] : (uint64_t)i * stride;
+		const uint64_t fio = iomap_base + o;
+		struct ixg_bsys_desc d;
+		if (r->verdict == IXG_V_UDP) {
+			d.sysnr = IXG_USYS_UDP_RECV;
+			d.arga = fio + r->l4_off;
+			d.argb = r->l4_len;
+			d.argc = fio;
+			d.argd = 0;
+			if (flags & IXG_EV_UDP_TUPLE) {
+				uint8_t *f = base + o;
+				const uint8_t *u = f + r->l4_off - 8;
+				uint32_t src = ((uint32_t)f[26] << 24) | ((uint32_t)f[27] << 16) | ((uint32_t)f[28] << 8) | f[29];
+				uint32_t dst = ((uint32_t)f[30] << 24) | ((uint32_t)f[31] << 16) | ((uint32_t)f[32] << 8) | f[33];
+				uint16_t sp = (uint16_t)((u[0] << 8) | u[1]), dp = (uint16_t)((u[2] << 8) | u[3]);
+				memcpy(f, &src, 4); /* id->src_ip = ntoh32(iphdr->src_addr.addr) */
+				memcpy(f + 4, &dst, 4);
+				memcpy(f + 8, &sp, 2); /* id->src_port = ntoh16(udphdr->src_port) */
+				memcpy(f + 10, &dp, 2);
+			}
+		} else if (r->verdict == IXG_V_TCP && dmx && dmx[i].kind == IXG_D_ACTIVE && r->l4_len > 0 &&
+			   dmx[i].id < n_pcbs) {
+			const struct ixg_ev_pcb *pc = &pcbs[dmx[i].id];
+			d.sysnr = IXG_USYS_TCP_RECV;
+			d.arga = (pc->pcb_idx & 0xffffffffffffull) | ((uint64_t)r->fg_id << 48);
+			d.argb = pc->cookie;
+			d.argc = fio + r->l4_off;
+			d.argd = r->l4_len;
+		} else {
+			continue;
+		}
+		ev[k] = d;
+		if (frame_idx)
+			frame_idx[k] = i;
+		k++;
+	}
+	return k;
+}

@@ -55,6 +55,8 @@ def lib() -> ctypes.CDLL:
         L.ixgo_pseudo_seed.restype = u16
         L.ixgo_tx_batch.argtypes = [vp, vp, u32, vp, vp, u32, u32, vp, vp]
         L.ixgo_tx_batch.restype = i32
+        L.ixgo_ev_batch.argtypes = [vp, vp, u32, vp, vp, vp, u32, u32, ctypes.c_uint64, u32, vp, vp]
+        L.ixgo_ev_batch.restype = u32
         _lib = L
     return _lib
 
@@ -183,3 +185,26 @@ def tx_batch(seg_buf: np.ndarray, segs: np.ndarray, src_mac: bytes, dmacs: np.nd
     L.ixgo_tx_batch(buf.ctypes.data, sg.ctypes.data, n, src.ctypes.data, d.ctypes.data, d.shape[0], flags,
                     out.ctypes.data, out_len.ctypes.data)
     return out, out_len
+
+
+EV_DTYPE = np.dtype([("sysnr", "<u8"), ("arga", "<u8"), ("argb", "<u8"), ("argc", "<u8"), ("argd", "<u8")])
+EV_PCB_DTYPE = np.dtype([("pcb_idx", "<u8"), ("cookie", "<u8")])
+
+
+def ev_batch(blob: np.ndarray, off, stride: int, rec: np.ndarray, dmx, pcbs, iomap_base: int, flags: int = 0):
+    """usys descriptors for a batch (oracle/ixgrx_oracle.c ixgo_ev_batch).
+    Returns (events, frame indices, the frames after the optional UDP tuple
+    writes)."""
+    L = lib()
+    b = np.ascontiguousarray(blob, dtype=np.uint8).copy()
+    n = int(rec.shape[0])
+    offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    r = np.ascontiguousarray(rec).view(np.uint8).reshape(n, 16)
+    d = None if dmx is None else np.ascontiguousarray(dmx).view(np.uint8).reshape(n, 8)
+    pc = np.ascontiguousarray(pcbs if pcbs is not None else np.zeros(0, EV_PCB_DTYPE), dtype=EV_PCB_DTYPE)
+    ev = np.zeros(max(n, 1), dtype=EV_DTYPE)
+    fi = np.zeros(max(n, 1), dtype=np.uint32)
+    k = L.ixgo_ev_batch(b.ctypes.data, None if offa is None else offa.ctypes.data, stride, r.ctypes.data,
+                        None if d is None else d.ctypes.data, pc.ctypes.data if pc.size else None, pc.size, n,
+                        iomap_base, flags, ev.ctypes.data, fi.ctypes.data)
+    return ev[:k].copy(), fi[:k].copy(), b

@@ -42,4 +42,11 @@ uint32_t ref_tcp_frame(uint32_t local_raw, uint32_t remote_raw, uint8_t tos, uin
 uint32_t ref_udp_frame(uint32_t src_raw, uint32_t dst_raw, uint16_t sport, uint16_t dport, const void *payload,
 		       uint16_t len, uint8_t *out);
 uint16_t ref_pseudo_seed(uint32_t src_raw, uint32_t dst_raw, uint8_t proto, uint16_t tot_len);
+
+/* event records: the reference's usys encoders and iomap */
+#include <stddef.h>
+void ref_ev_set_iomap(uint64_t iomap_offset);
+uint64_t ref_iomap(const void *p);
+void ref_ev_udp(void *addr, size_t len, void *id, uint64_t out[5]);
+void ref_ev_tcp(uint64_t handle, unsigned long cookie, void *addr, size_t len, uint64_t out[5]);
 #endif

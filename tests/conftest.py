@@ -18,11 +18,12 @@ def pytest_configure(config):
 
 def golden_names(prefix: str = ""):
     """RX fixtures by default; demux fixtures are the ones named demux_*, the
-    TX fixture is tx.npz (tests/test_tx.py)."""
+    TX fixture is tx.npz (tests/test_tx.py), the event fixture ev.npz
+    (tests/test_events.py)."""
     names = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
     if prefix:
         return [n for n in names if n.startswith(prefix)]
-    return [n for n in names if not n.startswith("demux") and n != "tx"]
+    return [n for n in names if not n.startswith("demux") and n not in ("tx", "ev")]
 
 
 def load_golden(name):
