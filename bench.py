@@ -216,6 +216,10 @@ def parity_leg(checks, key) -> dict:
             _, name, pool, flags, rec, tiled = c
             er, _ = oracle.rx_trace(pool, key, flags=flags, threads=8, hash_mode=oracle.HASH_TABLE)
             res[name] = "ok" if tiled and np.array_equal(rec, er) else "MISMATCH"
+        elif c[0] == "mbufs":
+            _, tr, ptrs, arena, rec = c
+            er = oracle.rx_mbufs(key, 128, 0, 0, ptrs[:1 << 16], threads=8, hash_mode=oracle.HASH_TABLE)
+            res["mbufs"] = "ok" if np.array_equal(rec.view(np.uint8).reshape(-1, 16)[:1 << 16], er) else "MISMATCH"
         elif c[0] == "tx":
             _, kind, (buf, segs, smac, dmacs, out, out_len), tiled = c
             size = int(segs["out_off"][-1]) + 2048
@@ -363,6 +367,28 @@ def tx_line(dev, steps: int, eng, kind: str, n: int):
             "parity": "tiled-consistent" if tiled else "MISMATCH"}, ("tx", kind, first, tiled)
 
 
+def mbuf_path(eng, n: int, seed: int, reps: int = 3):
+    """IX's own layout end to end: n C2 frames in 2112-byte
+    mbufs in host memory -> ixg_rx_batch_mbufs (gather into pinned staging,
+    H2D, kernels, D2H of records; pipelined in chunks over two stages) ->
+    records in host memory."""
+    from ix_amd import ixgrx, traces
+    tr = traces.make_trace("tcp64", n, seed=seed, pool=1 << 16)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    eng.batch_mbufs(ptrs[:1024])
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rec = eng.batch_mbufs(ptrs)
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    tiled = bool((rec.view(np.uint8).reshape(n // (1 << 16), -1) ==
+                  rec.view(np.uint8).reshape(n // (1 << 16), -1)[:1]).all())
+    return {"mpps": round(n / best / 1e6, 2), "seconds": round(best, 4), "frames": n,
+            "note": "host mbufs -> records in host memory, one host thread (IX's per-CPU model)",
+            "parity": "tiled-consistent" if tiled else "MISMATCH"}, ("mbufs", tr, ptrs, arena, rec)
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -474,6 +500,9 @@ def main():
             res["tx"][kind], tchk = tx_line(dev, max(5, args.steps // 2), engine(0), kind, n)
             checks.append(tchk)
             torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_copy and args.workload == "c2":
+        res["mbuf_path"], mchk = mbuf_path(engine(0), 1 << 21, seed=0x1BF000)
+        checks.append(mchk)
     if rank == 0 and world == 1 and not args.no_copy:
         del wl
         torch.cuda.empty_cache()
@@ -492,6 +521,8 @@ def main():
         if "demux" in res:
             res["demux"]["parity"] = par["demux"]
             res["demux"]["kinds"] = par["demux_kinds"]
+        if "mbuf_path" in res:
+            res["mbuf_path"]["parity"] = par["mbufs"] if res["mbuf_path"]["parity"] != "MISMATCH" else "MISMATCH"
         for kind in res.get("tx", {}):
             res["tx"][kind]["parity"] = par["tx_" + kind]
     if rank == 0:

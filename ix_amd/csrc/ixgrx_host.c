@@ -18,6 +18,32 @@
 #include "ixgrx_tx.h"
 #include "ixgrx_ev.h"
 
+/* per-launch kernel state that concurrent launches must not share: the
+ * defer flags and the class stamps */
+struct ixg_dstate {
+	uint8_t *d_defer;    /* one flag per 64-packet chunk */
+	size_t defer_cap;
+	uint32_t *d_present; /* [4] (ixg_kparams.present) */
+	uint32_t epoch;      /* last launch's stamp */
+};
+
+/* one stage of the pipelined host path (ixg_rx_batch_mbufs): pinned
+ * staging, device buffers, its own stream and defer state */
+#define IXG_SLOTS 2
+struct ixg_slot {
+	struct ixg_dstate ds;
+	hipStream_t stream;
+	hipEvent_t done;
+	int busy;            /* work enqueued, records not yet taken */
+	uint32_t first, n;   /* the chunk of the caller's batch it holds */
+	uint8_t *h_frames, *d_frames;
+	size_t frames_cap;
+	uint64_t *h_off, *d_off;
+	uint16_t *h_len, *d_len;
+	struct ixg_rx_rec *h_rec, *d_rec;
+	size_t n_cap;
+};
+
 struct ixg_ctx {
 	int device;
 	struct ixg_rx_cfg cfg;
@@ -26,20 +52,13 @@ struct ixg_ctx {
 	int force_general;   /* IXGRX_FORCE_GENERAL=1: skip the fixed-shape kernel (tests/A-B) */
 	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
 	uint32_t force_mode; /* IXGRX_MODE=fast|short|long: force the launch split (tests) */
-	uint8_t *d_defer;    /* one flag per 64-packet chunk */
+	struct ixg_dstate ds; /* the synchronous and device-resident paths' */
+	struct ixg_slot slot[IXG_SLOTS];
 	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
-	uint32_t *d_present; /* [3] per-class stamps (ixg_kparams.present) */
-	uint32_t epoch;      /* last launch's stamp */
-	size_t defer_cap;
 	uint64_t *d_tab;
 	uint32_t *d_tab6;
 	hipStream_t stream; /* for the synchronous host paths */
-	/* host-path staging */
-	uint8_t *h_frames;
-	size_t h_frames_cap;
-	uint64_t *h_off;
-	uint16_t *h_len;
-	size_t h_n_cap;
+	/* host-path device staging (ixg_rx_batch_host, ixg_demux_batch_host) */
 	uint8_t *d_frames;
 	size_t d_frames_cap;
 	uint64_t *d_off;
@@ -168,9 +187,28 @@ void ixg_rx_fini(void *vctx)
 		hipStreamSynchronize(c->stream);
 	hipFree(c->d_tab);
 	hipFree(c->d_tab6);
-	hipFree(c->d_defer);
+	hipFree(c->ds.d_defer);
 	hipFree(c->d_zero);
-	hipFree(c->d_present);
+	hipFree(c->ds.d_present);
+	for (int k = 0; k < IXG_SLOTS; k++) {
+		struct ixg_slot *sl = &c->slot[k];
+		if (sl->stream)
+			hipStreamSynchronize(sl->stream);
+		hipFree(sl->ds.d_defer);
+		hipFree(sl->ds.d_present);
+		hipHostFree(sl->h_frames);
+		hipHostFree(sl->h_off);
+		hipHostFree(sl->h_len);
+		hipHostFree(sl->h_rec);
+		hipFree(sl->d_frames);
+		hipFree(sl->d_off);
+		hipFree(sl->d_len);
+		hipFree(sl->d_rec);
+		if (sl->done)
+			hipEventDestroy(sl->done);
+		if (sl->stream)
+			hipStreamDestroy(sl->stream);
+	}
 	hipFree(c->d_dmacs);
 	hipFree(c->d_txbuf);
 	hipFree(c->d_txout);
@@ -188,9 +226,6 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_tw);
 	hipFree(c->d_listen);
 	hipFree(c->d_dmx);
-	hipHostFree(c->h_frames);
-	hipHostFree(c->h_off);
-	hipHostFree(c->h_len);
 	if (c->stream)
 		hipStreamDestroy(c->stream);
 	free(c);
@@ -269,8 +304,8 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 	}
 	if (hipMalloc((void **)&c->d_zero, IXG_ZERO_PAGE) != hipSuccess ||
 	    hipMemset(c->d_zero, 0, IXG_ZERO_PAGE) != hipSuccess ||
-	    hipMalloc((void **)&c->d_present, 4 * sizeof(uint32_t)) != hipSuccess ||
-	    hipMemset(c->d_present, 0, 4 * sizeof(uint32_t)) != hipSuccess)
+	    hipMalloc((void **)&c->ds.d_present, 4 * sizeof(uint32_t)) != hipSuccess ||
+	    hipMemset(c->ds.d_present, 0, 4 * sizeof(uint32_t)) != hipSuccess)
 		goto fail;
 	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
@@ -283,8 +318,9 @@ fail:
 
 /* ---- batches --------------------------------------------------------------- */
 
-static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
-		  uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum, hipStream_t s)
+static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
+		     const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
+		     hipStream_t s)
 {
 	struct ixg_kparams p;
 	memset(&p, 0, sizeof(p));
@@ -304,23 +340,29 @@ static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, c
 	p.zero = c->d_zero;
 	size_t nchunks = ((size_t)n + 63) / 64;
 	if (!c->force_general) {
-		if (nchunks > c->defer_cap) {
+		if (nchunks > ds->defer_cap) {
 			/* grows once per larger batch; not inside a graph capture */
-			hipFree(c->d_defer);
-			c->d_defer = NULL;
-			c->defer_cap = 0;
+			hipFree(ds->d_defer);
+			ds->d_defer = NULL;
+			ds->defer_cap = 0;
 			size_t cap = nchunks + nchunks / 4 + 64;
-			HIPCHK(hipMalloc((void **)&c->d_defer, cap));
-			c->defer_cap = cap;
+			HIPCHK(hipMalloc((void **)&ds->d_defer, cap));
+			ds->defer_cap = cap;
 		}
-		p.defer = c->d_defer;
-		p.present = c->d_present;
-		if (++c->epoch == 0)
-			c->epoch = 1;
-		p.epoch = c->epoch;
+		p.defer = ds->d_defer;
+		p.present = ds->d_present;
+		if (++ds->epoch == 0)
+			ds->epoch = 1;
+		p.epoch = ds->epoch;
 		p.force_mode = c->force_mode;
 	}
 	return ixgrx_launch(&p, c->fast_variant, c->ncu, s) == 0 ? 0 : -EIO;
+}
+
+static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
+		  uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum, hipStream_t s)
+{
+	return launch_ds(c, &c->ds, base, off, len, stride, n, out, csum, s);
 }
 
 int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
@@ -408,25 +450,45 @@ int ixg_rx_batch_host(void *vctx, const void *frames, const uint64_t *off, const
 	return 0;
 }
 
-static int grow_host(struct ixg_ctx *c, size_t bytes, size_t n)
+/* The IX-layout host path, pipelined: the batch goes
+ * through the device in chunks of at most IXG_PIPE_FRAMES frames /
+ * IXG_PIPE_BYTES bytes, alternating between IXG_SLOTS stages, so the CPU
+ * gathers chunk k+1 out of the mbufs into pinned staging while chunk k's
+ * H2D copy, kernels and D2H copy of records run on the stage's stream (and
+ * one stage's D2H overlaps the other's H2D). */
+#define IXG_PIPE_FRAMES 131072u
+#define IXG_PIPE_BYTES (64u << 20)
+
+static int slot_init(struct ixg_ctx *c, struct ixg_slot *sl)
 {
-	if (bytes > c->h_frames_cap) {
-		hipHostFree(c->h_frames);
-		c->h_frames = NULL;
-		size_t cap = bytes + bytes / 4 + 4096;
-		HIPCHK(hipHostMalloc((void **)&c->h_frames, cap, hipHostMallocDefault));
-		c->h_frames_cap = cap;
-	}
-	if (n > c->h_n_cap) {
-		hipHostFree(c->h_off);
-		hipHostFree(c->h_len);
-		c->h_off = NULL;
-		c->h_len = NULL;
-		size_t cap = n + n / 4 + 64;
-		HIPCHK(hipHostMalloc((void **)&c->h_off, cap * sizeof(uint64_t), hipHostMallocDefault));
-		HIPCHK(hipHostMalloc((void **)&c->h_len, cap * sizeof(uint16_t), hipHostMallocDefault));
-		c->h_n_cap = cap;
-	}
+	if (sl->stream)
+		return 0;
+	HIPCHK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
+	HIPCHK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
+	HIPCHK(hipMalloc((void **)&sl->ds.d_present, 4 * sizeof(uint32_t)));
+	HIPCHK(hipMemset(sl->ds.d_present, 0, 4 * sizeof(uint32_t)));
+	sl->frames_cap = IXG_PIPE_BYTES + IXG_TAIL_PAD;
+	sl->n_cap = IXG_PIPE_FRAMES;
+	HIPCHK(hipHostMalloc((void **)&sl->h_frames, sl->frames_cap, hipHostMallocDefault));
+	HIPCHK(hipHostMalloc((void **)&sl->h_off, sl->n_cap * sizeof(uint64_t), hipHostMallocDefault));
+	HIPCHK(hipHostMalloc((void **)&sl->h_len, sl->n_cap * sizeof(uint16_t), hipHostMallocDefault));
+	HIPCHK(hipHostMalloc((void **)&sl->h_rec, sl->n_cap * sizeof(struct ixg_rx_rec), hipHostMallocDefault));
+	HIPCHK(hipMalloc((void **)&sl->d_frames, sl->frames_cap));
+	HIPCHK(hipMalloc((void **)&sl->d_off, sl->n_cap * sizeof(uint64_t)));
+	HIPCHK(hipMalloc((void **)&sl->d_len, sl->n_cap * sizeof(uint16_t)));
+	HIPCHK(hipMalloc((void **)&sl->d_rec, sl->n_cap * sizeof(struct ixg_rx_rec)));
+	(void)c;
+	return 0;
+}
+
+/* wait for a stage's chunk and hand its records to the caller */
+static int slot_take(struct ixg_slot *sl, struct ixg_rx_rec *out)
+{
+	if (!sl->busy)
+		return 0;
+	HIPCHK(hipEventSynchronize(sl->done));
+	memcpy(out + sl->first, sl->h_rec, (size_t)sl->n * sizeof(*out));
+	sl->busy = 0;
 	return 0;
 }
 
@@ -437,42 +499,65 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 		return -EINVAL;
 	if (n == 0)
 		return 0;
-	/* gather: frame = mbuf + 64, L = mbuf->len (size_t @0), inc/ix/mbuf.h:73-90 */
-	size_t total = 0;
 	for (uint32_t i = 0; i < n; i++) {
 		size_t l;
 		memcpy(&l, mbufs[i], sizeof(l));
 		if (l > 0xffff)
 			return -EINVAL;
-		total += (l + 3) & ~(size_t)3;
 	}
 	HIPCHK(hipSetDevice(c->device));
-	int rc = grow_host(c, total + IXG_TAIL_PAD, n);
-	if (!rc)
-		rc = grow_dev(c, total + IXG_TAIL_PAD, n);
-	if (rc)
-		return rc;
-	size_t o = 0;
-	for (uint32_t i = 0; i < n; i++) {
-		const uint8_t *m = (const uint8_t *)mbufs[i];
-		size_t l;
-		memcpy(&l, m, sizeof(l));
-		memcpy(c->h_frames + o, m + IXG_MBUF_HEADER_LEN, l);
-		memset(c->h_frames + o + l, 0, ((l + 3) & ~(size_t)3) - l);
-		c->h_off[i] = o;
-		c->h_len[i] = (uint16_t)l;
-		o += (l + 3) & ~(size_t)3;
+	int rc = 0;
+	uint32_t i = 0, k = 0;
+	while (i < n && !rc) {
+		struct ixg_slot *sl = &c->slot[k % IXG_SLOTS];
+		if ((rc = slot_init(c, sl)) || (rc = slot_take(sl, out)))
+			break;
+		/* gather: frame = mbuf + 64, L = mbuf->len (size_t @0), inc/ix/mbuf.h:73-90 */
+		size_t o = 0;
+		uint32_t m = 0;
+		while (i + m < n && m < IXG_PIPE_FRAMES) {
+			const uint8_t *mb = (const uint8_t *)mbufs[i + m];
+			size_t l;
+			memcpy(&l, mb, sizeof(l));
+			const size_t sz = (l + 3) & ~(size_t)3;
+			if (o + sz > IXG_PIPE_BYTES)
+				break;
+			memcpy(sl->h_frames + o, mb + IXG_MBUF_HEADER_LEN, l);
+			memset(sl->h_frames + o + l, 0, sz - l);
+			sl->h_off[m] = o;
+			sl->h_len[m] = (uint16_t)l;
+			o += sz;
+			m++;
+		}
+		memset(sl->h_frames + o, 0, IXG_TAIL_PAD);
+		hipStream_t s = sl->stream;
+		if (hipMemcpyAsync(sl->d_frames, sl->h_frames, o + IXG_TAIL_PAD, hipMemcpyHostToDevice, s) != hipSuccess ||
+		    hipMemcpyAsync(sl->d_off, sl->h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, s) != hipSuccess ||
+		    hipMemcpyAsync(sl->d_len, sl->h_len, m * sizeof(uint16_t), hipMemcpyHostToDevice, s) != hipSuccess) {
+			rc = -EIO;
+			break;
+		}
+		if ((rc = launch_ds(c, &sl->ds, sl->d_frames, sl->d_off, sl->d_len, 0, m, sl->d_rec, NULL, s)))
+			break;
+		if (hipMemcpyAsync(sl->h_rec, sl->d_rec, m * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s) !=
+			    hipSuccess ||
+		    hipEventRecord(sl->done, s) != hipSuccess) {
+			rc = -EIO;
+			break;
+		}
+		sl->first = i;
+		sl->n = m;
+		sl->busy = 1;
+		i += m;
+		k++;
 	}
-	memset(c->h_frames + o, 0, IXG_TAIL_PAD);
-	HIPCHK(hipMemcpyAsync(c->d_frames, c->h_frames, o + IXG_TAIL_PAD, hipMemcpyHostToDevice, c->stream));
-	HIPCHK(hipMemcpyAsync(c->d_off, c->h_off, n * sizeof(uint64_t), hipMemcpyHostToDevice, c->stream));
-	HIPCHK(hipMemcpyAsync(c->d_len, c->h_len, n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
-	rc = launch(c, c->d_frames, c->d_off, c->d_len, 0, n, c->d_out, NULL, c->stream);
-	if (rc)
-		return rc;
-	HIPCHK(hipMemcpyAsync(out, c->d_out, n * sizeof(*out), hipMemcpyDeviceToHost, c->stream));
-	HIPCHK(hipStreamSynchronize(c->stream));
-	return 0;
+	/* drain, oldest stage first */
+	for (uint32_t t = 0; t < IXG_SLOTS; t++) {
+		int r2 = slot_take(&c->slot[(k + t) % IXG_SLOTS], out);
+		if (!rc)
+			rc = r2;
+	}
+	return rc;
 }
 
 /* ---- dispatch: what eth_process_recv does per packet, from records ------ */

@@ -208,6 +208,12 @@ def make_mbufs(tr) -> tuple[np.ndarray, np.ndarray]:
     n = tr.n
     arena = np.zeros(n * 2112 + 64, dtype=np.uint8)
     base = (-arena.ctypes.data) % 64
+    if tr.off is None and n and (tr.len == tr.len[0]).all():  # fixed stride, one length: vectorised
+        L = int(tr.len[0])
+        rows = arena[base:base + n * 2112].reshape(n, 2112)
+        rows[:, :8] = np.frombuffer(np.uint64(L).tobytes(), np.uint8)
+        rows[:, 64:64 + L] = tr.blob[:n * tr.stride].reshape(n, tr.stride)[:, :L]
+        return arena, arena.ctypes.data + base + np.arange(n, dtype=np.uint64) * 2112
     offs = tr.offsets()
     for i in range(n):
         o = base + i * 2112

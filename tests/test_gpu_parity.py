@@ -115,6 +115,20 @@ def test_mbuf_path(engines):
     _diff(rec, er, "mbufs")
 
 
+@pytest.mark.parametrize("kind,n", [("imix", 150000), ("tcp1514", 50000)])
+def test_mbuf_path_pipelined(kind, n, engines):
+    """A batch larger than one pipeline chunk (131072 frames / 64 MiB): the
+    chunks go through the two stages in turn and records land in order."""
+    tr = traces.make_trace(kind, n, seed=22, bad_ip=0.01, bad_l4=0.01)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    eng = engines()
+    rec = eng.batch_mbufs(ptrs)
+    er = oracle.rx_mbufs(KEY, 128, 0, 0, ptrs, threads=8)
+    _diff(rec, er, "mbufs pipelined")
+    rec2 = eng.batch_mbufs(ptrs[: n // 3])  # the stages are reusable, and a short batch after a long one
+    _diff(rec2, er[: n // 3], "mbufs pipelined, second call")
+
+
 @pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 256, 257, 1000, 4097])
 def test_ragged_sizes(n, engines):
     tr = traces.make_trace("mixed", n, seed=n)
