@@ -73,8 +73,16 @@ struct WaveTx {
   lds_u32* hdr;    // [kHdr][64]
 };
 
-// Pass A: lane = segment. Returns the frame's piece count K (0 if invalid).
-DEV uint32_t tx_prepare(const TParams& p, uint32_t i, int lane, const WaveTx& w) {
+// Pass A's result for one segment (lane = segment)
+struct Seg {
+  uint32_t h[kHdr];
+  uint64_t sa, oa;  // segment and frame addresses
+  uint32_t K, seg_len, term;
+  bool valid, udp, full;
+};
+
+// Pass A: lane = segment: descriptor, header dwords, checksum terms.
+DEV Seg tx_prepare(const TParams& p, uint32_t i) {
   const bool in = i < p.n;
   const uint32_t* dp = reinterpret_cast<const uint32_t*>(p.segs + (in ? i : 0u));
   const u32x4 a = *reinterpret_cast<const u32x4_a4*>(dp);
@@ -93,7 +101,8 @@ DEV uint32_t tx_prepare(const TParams& p, uint32_t i, int lane, const WaveTx& w)
   const bool offload = (p.flags & IXG_TX_OFFLOAD) != 0u;
   // the header, dwords of frame bytes 0..43 (ip_send_one + tcp_output_packet
   // / ip_setup_header + udp_output)
-  uint32_t h[kHdr];
+  Seg sg;
+  uint32_t (&h)[kHdr] = sg.h;
   h[0] = dm.x;
   h[1] = (dm.y & 0xffffu) | (p.smac_lo << 16);
   h[2] = (p.smac_lo >> 16) | (p.smac_hi << 16);
@@ -123,20 +132,28 @@ DEV uint32_t tx_prepare(const TParams& p, uint32_t i, int lane, const WaveTx& w)
     // pseudo header as inet_chksum_pseudo_partial adds it (:454-472, :436-437)
     term = (src & 0xffffu) + (src >> 16) + (dst & 0xffffu) + (dst >> 16) + (6u << 8) + bswap16(seg_len);
   }
-  const uint32_t K = valid ? (flen + 15u) >> 4 : 0u;
-  const uint64_t sa = reinterpret_cast<uint64_t>(p.seg_buf) + seg_off;
-  const uint64_t oa = reinterpret_cast<uint64_t>(p.out) + out_off;
-  w.src_lo[lane] = (uint32_t)sa;
-  w.src_hi[lane] = (uint32_t)(sa >> 32);
-  w.out_lo[lane] = (uint32_t)oa;
-  w.out_hi[lane] = (uint32_t)(oa >> 32);
-  w.meta[lane] = K | (udp ? 1u << 16 : 0u) | (valid ? 1u << 17 : 0u) | (tcp && !offload ? 1u << 18 : 0u);
-  w.seg_len[lane] = seg_len;
-  w.l4term[lane] = term;
-#pragma unroll
-  for (int k = 0; k < kHdr; k++) w.hdr[k * 64 + lane] = h[k];
+  sg.K = valid ? (flen + 15u) >> 4 : 0u;
+  sg.sa = reinterpret_cast<uint64_t>(p.seg_buf) + seg_off;
+  sg.oa = reinterpret_cast<uint64_t>(p.out) + out_off;
+  sg.seg_len = seg_len;
+  sg.term = term;
+  sg.valid = valid;
+  sg.udp = udp;
+  sg.full = tcp && !offload;
   if (in) p.out_len[i] = (uint16_t)(valid ? flen : 0u);
-  return K;
+  return sg;
+}
+
+DEV void tx_publish(const Seg& sg, int lane, const WaveTx& w) {
+  w.src_lo[lane] = (uint32_t)sg.sa;
+  w.src_hi[lane] = (uint32_t)(sg.sa >> 32);
+  w.out_lo[lane] = (uint32_t)sg.oa;
+  w.out_hi[lane] = (uint32_t)(sg.oa >> 32);
+  w.meta[lane] = sg.K | (sg.udp ? 1u << 16 : 0u) | (sg.valid ? 1u << 17 : 0u) | (sg.full ? 1u << 18 : 0u);
+  w.seg_len[lane] = sg.seg_len;
+  w.l4term[lane] = sg.term;
+#pragma unroll
+  for (int k = 0; k < kHdr; k++) w.hdr[k * 64 + lane] = sg.h[k];
 }
 
 DEV void store16(uint64_t addr, const u32x4& v) { *reinterpret_cast<u32x4*>(addr) = v; }
@@ -162,14 +179,18 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
     const int nr = valid ? (K - 2 + G - 1) / G : 0;  // output pieces 2..K-1
     uint64_t acc = 0;
     u32x4 held = {0u, 0u, 0u, 0u};
-    for (int r = 0; __any(r < nr); r++) {
+    const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
+    // always-issued loads (the zero page when there is nothing to read)
+    auto issue = [&](int r, u32x4& v, u32x4& vn) {
       const bool act = r < nr;
       const int j = G * r + t - 1;
-      // always-issued loads (the zero page when there is nothing to read)
-      const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
       const bool lo = act && j >= 0, ln = act && t == G - 1;
-      const u32x4 v = *reinterpret_cast<const u32x4_a4*>(lo ? src + 16u * (uint32_t)j : zero);
-      const u32x4 vn = *reinterpret_cast<const u32x4_a4*>(ln ? src + 16u * (uint32_t)(j + 1) : zero);
+      v = *reinterpret_cast<const u32x4_a4*>(lo ? src + 16u * (uint32_t)j : zero);
+      vn = *reinterpret_cast<const u32x4_a4*>(ln ? src + 16u * (uint32_t)(j + 1) : zero);
+    };
+    auto round = [&](int r, const u32x4& v, const u32x4& vn) {
+      const bool act = r < nr;
+      const int j = G * r + t - 1;
       const u32x4 own = j < 0 ? pm1 : v;
       u32x4 nxt;
       nxt.x = (uint32_t)__shfl_down((int)own.x, 1, G);
@@ -203,6 +224,14 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
         if (j == 0) sv.x &= 0xffff0000u;  // the checksum field (segment bytes 16..17) counts as 0
         acc += piece_sum(sv, seg_len - 16 * (j + 1));
       }
+    };
+    // two rounds' loads in flight per lane
+    for (int r = 0; __any(r < nr); r += 2) {
+      u32x4 v0, n0, v1, n1;
+      issue(r, v0, n0);
+      issue(r + 1, v1, n1);
+      round(r, v0, n0);
+      round(r + 1, v1, n1);
     }
     if (!udp) {
 #pragma unroll
@@ -221,12 +250,51 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
   }
 }
 
+// Every frame of the chunk fits 64 bytes (K <= 4: a TCP segment of at most
+// 30 bytes, a UDP payload of at most 22): lane = segment, all in registers.
+// Output pieces 0, 1 are header; piece 2 = header bytes [H-16, H) + body
+// piece 0, piece 3 = body pieces 0 and 1 (as in tx_stream, j = -1 and 0).
+DEV void tx_small(const TParams& p, const Seg& sg, int lane) {
+  const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
+  const u32x4 b0 = *reinterpret_cast<const u32x4_a4*>(sg.valid ? sg.sa : zero);
+  const u32x4 b1 = *reinterpret_cast<const u32x4_a4*>(sg.valid ? sg.sa + 16u : zero);
+  const uint32_t* h = sg.h;
+  u32x4 pm1, o2, o3;
+  if (sg.udp) {
+    pm1 = {mid(h[6], h[7]), mid(h[7], h[8]), mid(h[8], h[9]), mid(h[9], h[10])};
+    o2 = {mid(pm1.y, pm1.z), mid(pm1.z, pm1.w), mid(pm1.w, b0.x), mid(b0.x, b0.y)};
+    o3 = {mid(b0.y, b0.z), mid(b0.z, b0.w), mid(b0.w, b1.x), mid(b1.x, b1.y)};
+  } else {
+    pm1 = {mid(h[4], h[5]), mid(h[5], h[6]), mid(h[6], h[7]), mid(h[7], h[8])};
+    o2 = {mid(pm1.w, b0.x), mid(b0.x, b0.y), mid(b0.y, b0.z), mid(b0.z, b0.w)};
+    o3 = {mid(b0.w, b1.x), mid(b1.x, b1.y), mid(b1.y, b1.z), mid(b1.z, b1.w)};
+    const int L = (int)sg.seg_len;
+    u32x4 c1 = b1;
+    c1.x &= 0xffff0000u;  // the checksum field counts as 0
+    const uint64_t acc = piece_sum(b0, L) + piece_sum(c1, L - 16);
+    const uint32_t ck = sg.full ? (~fold16(acc + sg.term)) & 0xffffu : sg.term;
+    o3.x = (o3.x & 0xffffu) | (ck << 16);
+  }
+  if (sg.valid) {
+    store16(sg.oa, u32x4{h[0], h[1], h[2], h[3]});
+    store16(sg.oa + 16u, u32x4{h[4], h[5], h[6], h[7]});
+    store16(sg.oa + 32u, o2);
+    if (sg.K > 3u) store16(sg.oa + 48u, o3);
+  }
+}
+
 DEV void tx_loop(const TParams& p, const WaveTx& w) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
   for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < nchunks; c += nw) {
-    const uint32_t K = tx_prepare(p, c * 64u + (uint32_t)lane, lane, w);
+    const Seg sg = tx_prepare(p, c * 64u + (uint32_t)lane);
+    const uint32_t K = sg.K;
+    if (__all(K <= 4u)) {
+      tx_small(p, sg, lane);
+      continue;
+    }
+    tx_publish(sg, lane, w);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
