@@ -269,6 +269,13 @@ int ixg_demux_load(void *ctx, const struct ixg_demux_tables *t);
 int ixg_demux_batch_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec,
 			uint32_t n, struct ixg_demux_rec *d_out, void *stream);
 
+/* RX and demux in one pass (the demux fused into the RX kernels: the lookup
+ * runs from the parse state, with no second pass over frames or records):
+ * d_out as ixg_rx_batch_dev, d_dmx as ixg_demux_batch_dev. Asynchronous on
+ * `stream`. 0 or -errno (-ENOENT: no tables loaded). */
+int ixg_rx_demux_batch_dev(void *ctx, const struct ixg_rx_frames *frames, uint32_t n, struct ixg_rx_rec *d_out,
+			   struct ixg_demux_rec *d_dmx, void *stream);
+
 /* Host variant of ixg_demux_batch_dev (copies in, runs, copies out). */
 int ixg_demux_batch_host(void *ctx, const void *frames, const uint64_t *off, const uint16_t *len,
 			 uint32_t stride, uint32_t n, const struct ixg_rx_rec *rec,

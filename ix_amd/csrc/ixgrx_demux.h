@@ -18,6 +18,7 @@ struct ixg_dparams {
 	const struct ixg_rx_rec *rec;
 	struct ixg_demux_rec *out;
 	const uint32_t *active_start; /* nfg*512 + 1 */
+	const uint32_t *bline;        /* nfg*512 bucket lines (ixgrx_walk.h) */
 	const struct ixg_pcb_key *active;
 	const uint32_t *tw_start;     /* nfg + 1 */
 	const struct ixg_pcb_key *tw;

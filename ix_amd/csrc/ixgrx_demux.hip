@@ -17,6 +17,7 @@
 
 #include "../../include/ixgrx.h"
 #include "ixgrx_demux.h"
+#include "ixgrx_walk.h"
 
 #define DEV __device__ __forceinline__
 
@@ -59,21 +60,6 @@ DEV void load_item(const DParams& p, uint32_t chunk, int lane, Item& it) {
   it.h1 = *reinterpret_cast<const u32x4_a4*>(f + 28);
 }
 
-// tcp_input_find_list (tcp_in.c:122-143): the first entry of [s, e) whose
-// (remote port, local port, remote ip, local ip) equals the segment's
-DEV bool find_list(const ixg_pcb_key* __restrict__ ent, uint32_t s, uint32_t e, uint32_t sport, uint32_t dport,
-                   uint32_t src, uint32_t dst, uint32_t& id) {
-  const uint32_t ports = sport | (dport << 16);
-  for (uint32_t k = s; k < e; k++) {
-    const u32x4 v = reinterpret_cast<const u32x4*>(ent)[k];
-    if (v.z == ports && v.x == src && v.y == dst) {
-      id = v.w;
-      return true;
-    }
-  }
-  return false;
-}
-
 template <bool OFFS>
 DEV void walk_item(const DParams& p, uint32_t i, const Item& it) {
   const uint32_t verdict = (it.rec.x >> 16) & 0xffu;
@@ -97,36 +83,8 @@ DEV void walk_item(const DParams& p, uint32_t i, const Item& it) {
       dw = v.y & 0xffffu;
     }
     const uint32_t sport = bswap16(sw), dport = bswap16(dw);  // tcp_in.c:230-231
-    bool hit = false;
-    if (fg < p.nfg) {
-      const uint32_t a = fg * IXG_PCB_BUCKETS + bucket;
-      hit = find_list(p.active, p.active_start[a], p.active_start[a + 1], sport, dport, src, dst, id);
-      if (hit) {
-        kind = IXG_D_ACTIVE;  // tcp_in.c:249-256
-      } else if (find_list(p.tw, p.tw_start[fg], p.tw_start[fg + 1], sport, dport, src, dst, id)) {
-        kind = IXG_D_TIMEWAIT;  // tcp_in.c:260-269
-        hit = true;
-      }
-    }
-    if (!hit) {
-      // tcp_in.c:273-304 without SO_REUSE / LWIP_IPV6 (opt.h:1579,2016):
-      // break at the first lpcb on the port whose address is the segment's
-      // destination or ANY; the hlist loop variable keeps the last entry
-      // when nothing breaks, so a non-empty list always yields an lpcb
-      if (p.n_listen != 0) {
-        uint32_t k = 0;
-        for (; k < p.n_listen; k++) {
-          const u32x4 v = reinterpret_cast<const u32x4*>(p.listen)[k];
-          if ((v.y & 0xffffu) == dport && (v.x == dst || v.x == 0u)) break;
-        }
-        if (k == p.n_listen) k = p.n_listen - 1;
-        id = reinterpret_cast<const u32x4*>(p.listen)[k].z;
-        kind = IXG_D_LISTEN;  // tcp_in.c:317-323
-      } else {
-        kind = (tflags & 0x04u) ? IXG_D_DROP : IXG_D_RESET;  // tcp_in.c:500-510 (TCP_RST = 0x04)
-        id = 0;
-      }
-    }
+    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
+    ixgwalk::walk(t, fg, bucket, tflags, src, dst, sport | (dport << 16), id, kind);
   }
   const u32x2 o = {id, kind};
   reinterpret_cast<u32x2*>(p.out)[i] = o;

@@ -72,6 +72,7 @@ struct ixg_ctx {
 	uint32_t *d_astart, *d_twstart;
 	struct ixg_pcb_key *d_active, *d_tw;
 	struct ixg_listen_key *d_listen;
+	uint32_t *d_bline;           /* nfg*512 bucket lines of 64 B (ixgrx_walk.h) */
 	struct ixg_demux_rec *d_dmx; /* host-path output staging */
 	size_t d_dmx_cap;
 	/* TX (ixg_tx_set_macs) */
@@ -210,6 +211,7 @@ void ixg_rx_fini(void *vctx)
 			hipStreamDestroy(sl->stream);
 	}
 	hipFree(c->d_dmacs);
+	hipFree(c->d_bline);
 	hipFree(c->d_txbuf);
 	hipFree(c->d_txout);
 	hipFree(c->d_txsegs);
@@ -320,7 +322,7 @@ fail:
 
 static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		     const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
-		     hipStream_t s)
+		     struct ixg_demux_rec *dmx, hipStream_t s)
 {
 	struct ixg_kparams p;
 	memset(&p, 0, sizeof(p));
@@ -338,6 +340,17 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
 	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
 	p.zero = c->d_zero;
+	if (dmx) {
+		p.dmx = dmx;
+		p.active_start = c->d_astart;
+		p.bline = c->d_bline;
+		p.active = c->d_active;
+		p.tw_start = c->d_twstart;
+		p.tw = c->d_tw;
+		p.listen = c->d_listen;
+		p.nfg = c->dmx_nfg;
+		p.n_listen = c->dmx_nlisten;
+	}
 	size_t nchunks = ((size_t)n + 63) / 64;
 	if (!c->force_general) {
 		if (nchunks > ds->defer_cap) {
@@ -362,7 +375,7 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
 		  uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum, hipStream_t s)
 {
-	return launch_ds(c, &c->ds, base, off, len, stride, n, out, csum, s);
+	return launch_ds(c, &c->ds, base, off, len, stride, n, out, csum, NULL, s);
 }
 
 int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
@@ -537,7 +550,7 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 			rc = -EIO;
 			break;
 		}
-		if ((rc = launch_ds(c, &sl->ds, sl->d_frames, sl->d_off, sl->d_len, 0, m, sl->d_rec, NULL, s)))
+		if ((rc = launch_ds(c, &sl->ds, sl->d_frames, sl->d_off, sl->d_len, 0, m, sl->d_rec, NULL, NULL, s)))
 			break;
 		if (hipMemcpyAsync(sl->h_rec, sl->d_rec, m * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s) !=
 			    hipSuccess ||
@@ -641,6 +654,23 @@ int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
 	    (rc = upload((void **)&c->d_tw, t->tw, ntw * sizeof(struct ixg_pcb_key))) ||
 	    (rc = upload((void **)&c->d_listen, t->listen, (size_t)t->n_listen * sizeof(struct ixg_listen_key))))
 		return rc;
+	/* the bucket lines (ixgrx_walk.h): count, CSR start, the first
+	 * IXG_BUCKET_INLINE entries of each active list, in list order */
+	uint32_t *bl = (uint32_t *)calloc(na_rows ? na_rows : 1, 64);
+	if (!bl)
+		return -ENOMEM;
+	for (size_t r = 0; r < na_rows; r++) {
+		const uint32_t s0 = t->active_start[r], cnt = t->active_start[r + 1] - s0;
+		uint32_t *row = bl + 16 * r;
+		row[0] = cnt;
+		row[1] = s0;
+		for (uint32_t k = 0; k < cnt && k < 3; k++)
+			memcpy(row + 4 + 4 * k, &t->active[s0 + k], sizeof(struct ixg_pcb_key));
+	}
+	rc = upload((void **)&c->d_bline, bl, na_rows * 64);
+	free(bl);
+	if (rc)
+		return rc;
 	c->dmx_nfg = t->nfg;
 	c->dmx_nlisten = t->n_listen;
 	c->demux_loaded = 1;
@@ -657,6 +687,7 @@ static int demux_launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *
 	p.rec = rec;
 	p.out = out;
 	p.active_start = c->d_astart;
+	p.bline = c->d_bline;
 	p.active = c->d_active;
 	p.tw_start = c->d_twstart;
 	p.tw = c->d_tw;
@@ -684,6 +715,25 @@ int ixg_demux_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
 	return demux_launch(c, (const uint8_t *)fr->base, fr->off, fr->stride, n, d_rec, d_out, (hipStream_t)stream);
+}
+
+int ixg_rx_demux_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
+			   struct ixg_demux_rec *d_dmx, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || (n && (!fr->base || !fr->len || !d_out || !d_dmx)))
+		return -EINVAL;
+	if (!c->demux_loaded)
+		return -ENOENT;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)fr->base & 3) || (!fr->off && (fr->stride & 3)) || ((uintptr_t)d_out & 15) ||
+	    ((uintptr_t)fr->len & 1) || ((uintptr_t)fr->off & 7) || ((uintptr_t)d_dmx & 7))
+		return -EINVAL;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -EIO;
+	return launch_ds(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, d_dmx,
+			 (hipStream_t)stream);
 }
 
 int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, const uint16_t *len, uint32_t stride,

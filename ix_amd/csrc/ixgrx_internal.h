@@ -37,6 +37,16 @@ struct ixg_kparams {
 	uint32_t epoch;        /* per-launch stamp (never 0) */
 	uint32_t force_mode;   /* IXG_MODE_* for the sampler to write instead of
 	                          sampling (tests), or IXG_MODE_AUTO */
+	/* fused PCB demux (ixg_rx_demux_batch_dev): dmx != NULL turns it on */
+	struct ixg_demux_rec *dmx;
+	const uint32_t *active_start;
+	const uint32_t *bline;        /* nfg*512 bucket lines (ixgrx_walk.h) */
+	const struct ixg_pcb_key *active;
+	const uint32_t *tw_start;
+	const struct ixg_pcb_key *tw;
+	const struct ixg_listen_key *listen;
+	uint32_t nfg;
+	uint32_t n_listen;
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
 };

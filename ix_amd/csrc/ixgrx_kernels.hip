@@ -29,6 +29,7 @@
 
 #include "../../include/ixgrx.h"
 #include "ixgrx_internal.h"
+#include "ixgrx_walk.h"
 
 #define DEV __device__ __forceinline__
 
@@ -218,6 +219,8 @@ struct LaneState {
   // fields the deferred verdict needs
   uint32_t l4, l4len, proto, doff, ulen, icmp_type;
   bool v6;
+  // the 4-tuple for the fused demux: raw IPs, ports host order (sport | dport << 16)
+  uint32_t src, dst, ports;
 };
 
 // FIXED: every lane is IPv4 with ihl 5 (wave-uniform), so the header
@@ -277,6 +280,9 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
 
   s.v6 = v6;
   s.proto = v6 ? byte_at(d, 20) : proto;
+  s.src = src;
+  s.dst = dst;
+  s.ports = ((b0 << 8) | b1) | (((b2 << 8) | b3) << 16);
   const uint32_t v6_plen = (byte_at(d, 18) << 8) | byte_at(d, 19);
   const bool v6_ok = v6 && L >= 54 && (vh >> 4) == 6 && 54 + v6_plen <= L;
 
@@ -484,6 +490,20 @@ DEV void store_record(const KParams& p, uint32_t i, const Rec& r, uint32_t ip_re
   if (p.csum) p.csum[i] = ip_res | (l4_res << 16);
 }
 
+// Fused PCB demux (ixg_rx_demux_batch_dev): the tcp_input lookup of an
+// IXG_V_TCP record straight from the parse state, no second pass over the
+// frames or the records (ixgrx_walk.h; dp/net/tcp_in.c:233-323, 500-510).
+DEV void store_demux(const KParams& p, uint32_t i, const Rec& r, uint32_t src, uint32_t dst, uint32_t ports) {
+  if (!p.dmx) return;
+  uint32_t id = 0, kind = IXG_D_NONE;
+  if (((r.w0 >> 16) & 0xffu) == IXG_V_TCP) {
+    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
+    ixgwalk::walk(t, (r.w0 & 0xffffu) - p.fg_base, r.w3 & 0xffffu, (r.w3 >> 16) & 0xffu, src, dst, ports, id, kind);
+  }
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  reinterpret_cast<u32x2v*>(p.dmx)[i] = u32x2v{id, kind};
+}
+
 // Frame i's byte offset. The layout (u64 offsets vs fixed stride) is a
 // template parameter, not a runtime branch: a branch on p.off makes hipcc
 // join the two paths with a conservative s_waitcnt vmcnt(0) that drains
@@ -519,7 +539,9 @@ DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t
   lane_parse<true, kFastDw>(p, T, d, L, s);
   if (valid) {
     const uint32_t r4 = l4_residual(s);
-    store_record(p, i, make_record<true>(p, d, L, s, r4), s.ip_res, r4);
+    const Rec r = make_record<true>(p, d, L, s, r4);
+    store_record(p, i, r, s.ip_res, r4);
+    store_demux(p, i, r, s.src, s.dst, s.ports);
   }
 }
 
@@ -683,7 +705,9 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   if (SHORT || !m) {  // no long segment in this chunk (wave-uniform)
     if (valid) {
       const uint32_t r4 = l4_residual(s);
-      store_record(p, i, make_record(p, d, L, s, r4), s.ip_res, r4);
+      const Rec r = make_record(p, d, L, s, r4);
+      store_record(p, i, r, s.ip_res, r4);
+      store_demux(p, i, r, s.src, s.dst, s.ports);
     }
     return false;
   }
@@ -693,12 +717,14 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   Rec rok = make_record(p, d, L, s, r4);
   Rec rbad = make_record(p, d, L, s, 1u);
   uint32_t acc32 = fold32(s.l4_acc), ip_res = s.ip_res;
+  uint32_t tsrc = s.src, tdst = s.dst, tports = s.ports;
   const u32x4 ve = load16(lng && rr != 0u, p.base + off + pend, p.zero + 16 * lane);
   // materialise these now, so the parse state (d[], s) is dead during the
   // streaming rounds instead of being kept live for sunk computations
   asm volatile("" : "+v"(rok.w0), "+v"(rok.w1), "+v"(rok.w2), "+v"(rok.w3));
   asm volatile("" : "+v"(rbad.w0), "+v"(rbad.w1), "+v"(rbad.w2), "+v"(rbad.w3));
   asm volatile("" : "+v"(acc32), "+v"(ip_res));
+  asm volatile("" : "+v"(tsrc), "+v"(tdst), "+v"(tports));
   if (lng) {
     w.list[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)lane;
     w.end[lane] = pend;
@@ -723,8 +749,10 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
       const uint32_t end_piece = fold32(piece_sum(ve, (int)rr));
       const uint32_t res = (~fold16(add1c(add1c(acc32, w.sum[lane]), end_piece))) & 0xffffu;
       store_record(p, i, res == 0 ? rok : rbad, ip_res, res);
+      store_demux(p, i, res == 0 ? rok : rbad, tsrc, tdst, tports);
     } else {
       store_record(p, i, rok, ip_res, r4);
+      store_demux(p, i, rok, tsrc, tdst, tports);
     }
   }
   return false;

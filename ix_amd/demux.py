@@ -31,7 +31,7 @@ D_NONE, D_ACTIVE, D_TIMEWAIT, D_LISTEN, D_RESET, D_DROP = range(6)
 KINDS = {D_NONE: "NONE", D_ACTIVE: "ACTIVE", D_TIMEWAIT: "TIMEWAIT", D_LISTEN: "LISTEN", D_RESET: "RESET",
          D_DROP: "DROP"}
 BUCKETS = 512
-EXPORTS = ("ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host")
+EXPORTS = ("ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg_rx_demux_batch_dev")
 
 
 class _Tables(ctypes.Structure):
@@ -50,6 +50,8 @@ def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     lib.ixg_demux_batch_dev.restype = i32
     lib.ixg_demux_batch_host.argtypes = [vp, vp, vp, vp, u32, u32, vp, vp]
     lib.ixg_demux_batch_host.restype = i32
+    lib.ixg_rx_demux_batch_dev.argtypes = [vp, ctypes.POINTER(ixgrx.RxFrames), u32, vp, vp, vp]
+    lib.ixg_rx_demux_batch_dev.restype = i32
     lib._ixg_demux_bound = True
     return lib
 
@@ -145,6 +147,16 @@ def batch_dev(eng: ixgrx.RxEngine, base: int, off: int | None, stride: int, n: i
     fr = ixgrx.RxFrames(base, off or None, 0, stride, 0)
     ixgrx._check(lib.ixg_demux_batch_dev(eng._ctx, ctypes.byref(fr), rec, n, out, stream or None),
                  "ixg_demux_batch_dev", lib)
+
+
+def rx_demux_dev(eng: ixgrx.RxEngine, base: int, off: int | None, length: int, stride: int, n: int, rec: int,
+                 out: int, stream: int | None = None) -> None:
+    """RX and demux in one pass on the device (the demux fused into the RX
+    kernels): records into `rec`, demux records into `out`."""
+    lib = _bind(eng._lib)
+    fr = ixgrx.RxFrames(base, off or None, length, stride, 0)
+    ixgrx._check(lib.ixg_rx_demux_batch_dev(eng._ctx, ctypes.byref(fr), n, rec, out, stream or None),
+                 "ixg_rx_demux_batch_dev", lib)
 
 
 def batch_host(eng: ixgrx.RxEngine, blob: np.ndarray, off, lens: np.ndarray, stride: int,

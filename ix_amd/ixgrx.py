@@ -46,7 +46,7 @@ RF_IP_CSUM_CHECKED, RF_IP_CSUM_OK, RF_L4_CSUM_CHECKED, RF_L4_CSUM_OK, RF_RSS = 1
 EXPORTS = (
     "ixg_rx_init", "ixg_rx_fini", "ixg_rx_batch_dev", "ixg_rx_batch_mbufs", "ixg_rx_batch_host",
     "ixg_rx_hash_tables", "ixg_abi_version", "ixg_strerror", "ixg_rx_dispatch",
-    "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host",
+    "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg_rx_demux_batch_dev",
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
     "ixg_ev_batch_dev",
 )

@@ -187,3 +187,75 @@ def test_gpu_demux_requires_tables():
                              np.zeros(1, ixgrx.REC_DTYPE))
     finally:
         eng.close()
+
+
+def _engine_in_mode(cfg, mode):
+    """An engine with the launch split forced (IXGRX_MODE / IXGRX_FORCE_GENERAL)."""
+    import os
+    env = {"IXGRX_FORCE_GENERAL": "1" if mode == "general" else "0",
+           "IXGRX_MODE": mode if mode in ("fast", "short", "long") else "auto"}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return ixgrx.RxEngine(cfg)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _fused_dev(eng, blob, off, lens, stride, n):
+    import torch
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(np.concatenate([blob, np.zeros(64, np.uint8)])).to(dev)
+    tl = torch.from_numpy(np.ascontiguousarray(lens).view(np.int16)).to(dev)
+    to = None if off is None else torch.from_numpy(np.ascontiguousarray(off).view(np.int64)).to(dev)
+    rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    out = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    demux.rx_demux_dev(eng, tb.data_ptr(), None if to is None else to.data_ptr(), tl.data_ptr(), stride, n,
+                       rec.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return rec.cpu().numpy(), out.cpu().numpy()
+
+
+MODES = ["auto", "general", "fast", "short", "long"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+def test_gpu_fused_golden(golden_demux, mode):
+    """RX + demux in one pass (ixg_rx_demux_batch_dev) on the reference's
+    demux fixtures, every launch split."""
+    g = golden_demux
+    eng = _engine_in_mode(ixgrx.Config(bytes(g["key"]), int(g["nb_rx_fgs"]), int(g["dev_idx"]), 0), mode)
+    try:
+        demux.load(eng, _tables(g))
+        rec, out = _fused_dev(eng, g["blob"], g["off"], g["len"], 0, len(g["len"]))
+        assert (rec == g["rec"]).all()
+        _diff(out, g["demux"], g["name"] + " fused " + mode)
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("kind,n,listen", [("tcp64", 200000, True), ("imix", 100000, False),
+                                           ("mixed", 60000, True), ("tcp1514", 20000, True)])
+def test_gpu_fused_vs_oracle(kind, n, listen, mode):
+    rng = np.random.default_rng(n + 7)
+    tr = traces.make_trace(kind, n, seed=0x1BD100 + n, bad_ip=0.01, bad_l4=0.01)
+    cfg = ixgrx.Config(KEY, 128, 1, 0)
+    er, _ = oracle.rx_trace(tr, KEY, 128, 1, 0, threads=8, hash_mode=oracle.HASH_TABLE)
+    tabs = _synthetic_tables(cfg, tr, er, rng, listen=listen)
+    eng = _engine_in_mode(cfg, mode)
+    try:
+        demux.load(eng, tabs)
+        rec, out = _fused_dev(eng, tr.blob, tr.off, tr.len, tr.stride, tr.n)
+        assert (rec == er).all()
+        exp = oracle.demux_batch(tabs.nfg, tabs.active_start, tabs.active, tabs.tw_start, tabs.tw, tabs.listen,
+                                 512, tr.blob, tr.off, tr.len, tr.stride, er)
+        _diff(out, exp, f"{kind} fused {mode}")
+    finally:
+        eng.close()
