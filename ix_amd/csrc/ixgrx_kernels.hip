@@ -484,9 +484,16 @@ DEV Rec make_record(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t L
 
 DEV uint32_t l4_residual(const LaneState& s) { return s.l4_kind ? ((~fold16(s.l4_acc)) & 0xffffu) : 0xffffu; }
 
+// NT (the fixed-shape kernels): records are written once and not read back
+// by this launch, so streaming (non-temporal) stores -- 4% faster on C2 than
+// default-policy ones; the general kernels measured no gain
+template <bool NT = false>
 DEV void store_record(const KParams& p, uint32_t i, const Rec& r, uint32_t ip_res, uint32_t l4_res) {
   u32x4 w = {r.w0, r.w1, r.w2, r.w3};
-  *reinterpret_cast<u32x4*>(p.out + i) = w;
+  if (NT)
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p.out + i));
+  else
+    *reinterpret_cast<u32x4*>(p.out + i) = w;
   if (p.csum) p.csum[i] = ip_res | (l4_res << 16);
 }
 
@@ -540,7 +547,7 @@ DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t
   if (valid) {
     const uint32_t r4 = l4_residual(s);
     const Rec r = make_record<true>(p, d, L, s, r4);
-    store_record(p, i, r, s.ip_res, r4);
+    store_record<true>(p, i, r, s.ip_res, r4);
     store_demux(p, i, r, s.src, s.dst, s.ports);
   }
 }
@@ -940,7 +947,9 @@ DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t l
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t o = 16u * (uint32_t)(lane + 64 * k);
-    v[k] = *reinterpret_cast<const u32x4*>(cb + (o < top ? o : top));
+    // frames are read once: non-temporal loads (with the nt record stores,
+    // 7-8% on C2 over default-policy loads and stores)
+    v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(cb + (o < top ? o : top)));
   }
   const uint32_t i = cc * 64u + (uint32_t)lane;
   const uint32_t ic = i < p.n ? i : p.n - 1;
