@@ -32,12 +32,16 @@ PEAK_HBM_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # (which, when no chunk was deferred, only scans the per-chunk flags); the
 # HIP events bracket both on the launch stream
 def kernels(wl) -> str:
-    """The dispatches one launch makes (ixgrx_launch): the coalesced
-    fixed-shape kernel for fixed strides <= 64 B, else the lane-load one,
-    then the general kernel."""
+    """The dispatches one launch makes (ixgrx_launch): for fixed strides <=
+    64 B the coalesced fixed-shape kernel, else the sampler and the lane-load
+    one; then the short and the long general kernels (each exits at once
+    when its class has nothing deferred)."""
     if wl.off is not None:
-        return "ixg_rx_fast_o + ixg_rx_general_o"
-    return ("ixg_rx_fastc_s" if wl.stride <= 64 else "ixg_rx_fast_s") + " + ixg_rx_general_s"
+        return "ixg_rx_sample + ixg_rx_fast_o + ixg_rx_short_o + ixg_rx_general_o"
+    if wl.stride <= 64:
+        return "ixg_rx_fastc_s + ixg_rx_short_s + ixg_rx_general_s"
+    return "ixg_rx_sample + ixg_rx_fast_s + ixg_rx_short_s + ixg_rx_general_s"
+
 
 WORKLOADS = {
     # name: (trace kind, frames per GPU, distinct frames in the pool, description)

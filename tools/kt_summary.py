@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
 """Per-launch summary of a `rocprofv3 --kernel-trace --stats` run of bench.py.
 
-One ixg_rx_batch_dev launch = a fixed-shape dispatch (ixg_rx_fast_*) followed
-by a general dispatch (ixg_rx_general_*). bench.py's default command runs,
-in order: the primary workload (warmup + steps), the secondary workload
-(2 + max(5, steps/2)), then 3 copy-inclusive launches of the primary.
-This splits the trace into those phases and prints, per phase, the average
-per-kernel durations and the launch span (fast start -> general end), which
-is what the HIP events around each launch in bench.py measure.
+One RX launch (ixg_rx_batch_dev / ixg_rx_demux_batch_dev) is a short
+sequence of dispatches on one stream: [ixg_rx_sample] + a fixed-shape kernel
+(ixg_rx_fast*) + the short kernel (ixg_rx_short_*) + the long kernel
+(ixg_rx_general_*); kernels of a class with nothing to do exit at once. The
+demux, TX and event kernels are launches of their own. This groups the trace
+into launches, then into runs of consecutive launches with the same kernel
+sequence (bench.py's phases), and prints per run the launch count, the mean
+and min launch span (first dispatch start -> last dispatch end: what the HIP
+events around a launch measure) and the mean duration of each kernel.
 
-usage: kt_summary.py KT_DIR WARMUP STEPS [PRIMARY SECONDARY]
+usage: kt_summary.py KT_DIR
 """
 import csv
 import glob
@@ -18,46 +20,51 @@ import statistics
 import sys
 
 
-def main():
-    d, warm, steps = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
-    prim = sys.argv[4] if len(sys.argv) > 4 else "c2"
-    sec = sys.argv[5] if len(sys.argv) > 5 else "c4"
-    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
-    rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("ixg_rx")]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    launches = []
-    i = 0
-    while i < len(rows):
-        r = rows[i]
-        if "fast" in r["Kernel_Name"] and i + 1 < len(rows) and "general" in rows[i + 1]["Kernel_Name"]:
-            g = rows[i + 1]
-            launches.append((r, g))
-            i += 2
+def launches(rows):
+    out, cur = [], []
+    for r in rows:
+        n = r["Kernel_Name"]
+        if n.startswith("ixg_rx"):
+            if cur and (n == "ixg_rx_sample" or n.startswith("ixg_rx_fast")):
+                out.append(cur)
+                cur = []
+            cur.append(r)
+            if n.startswith("ixg_rx_general"):
+                out.append(cur)
+                cur = []
         else:
-            launches.append((None, r))
-            i += 1
-    s2 = max(5, steps // 2)
-    phases = [(f"{prim} warmup", warm), (f"{prim} timed", steps), (f"{sec} warmup", 2), (f"{sec} timed", s2),
-              (f"{prim} copy-inclusive", 3)]
-    out = ["| phase | launches | fast kernel avg us | general kernel avg us | launch span avg us | span min us |",
-           "|---|---|---|---|---|---|"]
-    k = 0
-    for name, cnt in phases:
-        ph = launches[k:k + cnt]
-        k += cnt
-        if not ph:
-            continue
+            if cur:
+                out.append(cur)
+                cur = []
+            out.append([r])
+    if cur:
+        out.append(cur)
+    return out
 
-        def dur(r):
-            return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        fa = [dur(a) for a, _ in ph if a is not None]
-        ga = [dur(b) for _, b in ph]
-        sp = [(int(b["End_Timestamp"]) - int((a or b)["Start_Timestamp"])) / 1e3 for a, b in ph]
-        kname = (ph[0][0] or ph[0][1])["Kernel_Name"]
-        out.append(f"| {name} ({kname}) | {len(ph)} | {statistics.mean(fa) if fa else 0:.1f} | "
-                   f"{statistics.mean(ga):.1f} | {statistics.mean(sp):.1f} | {min(sp):.1f} |")
-    if k != len(launches):
-        out.append(f"(trace holds {len(launches)} launches, phases account for {k})")
+
+def main():
+    d = sys.argv[1]
+    f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
+    rows = [r for r in csv.DictReader(open(f)) if r["Kernel_Name"].startswith("ixg_")]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    L = launches(rows)
+    runs = []
+    for ln in L:
+        key = tuple(r["Kernel_Name"] for r in ln)
+        if runs and runs[-1][0] == key:
+            runs[-1][1].append(ln)
+        else:
+            runs.append((key, [ln]))
+
+    def dur(r):
+        return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    out = ["| # | kernel sequence of a launch | launches | span mean us | span min us | per-kernel mean us |",
+           "|---|---|---|---|---|---|"]
+    for i, (key, lns) in enumerate(runs):
+        sp = [(int(ln[-1]["End_Timestamp"]) - int(ln[0]["Start_Timestamp"])) / 1e3 for ln in lns]
+        per = [statistics.mean(dur(ln[k]) for ln in lns) for k in range(len(key))]
+        out.append(f"| {i} | {' + '.join(key)} | {len(lns)} | {statistics.mean(sp):.1f} | {min(sp):.1f} | "
+                   f"{', '.join(f'{p:.1f}' for p in per)} |")
     print("\n".join(out))
 
 

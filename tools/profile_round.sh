@@ -13,12 +13,13 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 B="bench.py --steps 20 --warmup 5"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- python3 $B \
   > "$O/bench_under_rocprof.json" 2> "$O/kt.log" || { echo "kernel-trace run failed"; tail -20 "$O/kt.log"; exit 1; }
+python3 tools/kt_summary.py "$O/kt" > "$O/launch_summary.md" || exit 1
 du -sh "$O"/* ; find "$O" -size +1M -exec ls -la {} \;
 SPECS=""
 for W in c2 c4 c3 c5; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_${W}_$C" -o p -- python3 bench.py --workload $W \
-      --secondary '' --no-cpu --no-copy --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
+      --secondary '' --no-cpu --no-copy --no-demux --no-tx --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
       || { echo "pmc $W $C failed"; tail -20 "$O/pmc_${W}_$C.log"; exit 1; }
     find "$O/pmc_${W}_$C" -type f -exec ls -la {} \;
     [ -n "$(find "$O/pmc_${W}_$C" -name '*counter_collection.csv')" ] || { echo "no csv: $W $C"; tail -30 "$O/pmc_${W}_$C.log"; find "$O" -size +1M -delete; exit 1; }
