@@ -11,6 +11,9 @@ sequence (bench.py's phases), and prints per run the launch count, the mean
 and min launch span (first dispatch start -> last dispatch end: what the HIP
 events around a launch measure) and the mean duration of each kernel.
 
+The last phase of bench.py (the overlapped copy-inclusive leg) runs two
+streams, so its launches interleave and show up as short mixed runs.
+
 usage: kt_summary.py KT_DIR
 """
 import csv
@@ -25,7 +28,8 @@ def launches(rows):
     for r in rows:
         n = r["Kernel_Name"]
         if n.startswith("ixg_rx"):
-            if cur and (n == "ixg_rx_sample" or n.startswith("ixg_rx_fast")):
+            after_sampler = len(cur) == 1 and cur[0]["Kernel_Name"] == "ixg_rx_sample"
+            if cur and (n == "ixg_rx_sample" or (n.startswith("ixg_rx_fast") and not after_sampler)):
                 out.append(cur)
                 cur = []
             cur.append(r)
