@@ -59,6 +59,7 @@ typedef struct ixg_kparams ixg_kparams;
  * streaming), LONG = anything else */
 #define IXG_CLS_SHORT 1u
 #define IXG_CLS_LONG 2u
+#define IXG_CLS_ANY 3u   /* a long-kernel build that takes both classes */
 #define IXG_SHORT_MAX 112u
 
 /* how a launch splits the work, chosen on the device by the sampler kernel

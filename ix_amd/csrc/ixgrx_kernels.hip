@@ -1077,11 +1077,19 @@ DEV void general_body(const KParams& p) {
   // common case behind the fixed-shape kernel: 64 B frames)
   const uint32_t mode = launch_mode(p);
   const bool all = CLS == IXG_CLS_SHORT ? mode == IXG_MODE_SHORT : (p.defer == nullptr || mode == IXG_MODE_LONG);
-  if (!all && p.present[CLS] != p.epoch) return;  // nothing of this class deferred
+  // (p.present is only read when the flags are in use: it is null with
+  // p.defer when the general kernel runs alone)
+  if (!all) {
+    const bool stamped = CLS == IXG_CLS_ANY
+                             ? (p.present[IXG_CLS_SHORT] == p.epoch || p.present[IXG_CLS_LONG] == p.epoch)
+                             : p.present[CLS] == p.epoch;
+    if (!stamped) return;  // nothing of this class deferred
+  }
+  auto mine = [&](uint32_t ci) { return CLS == IXG_CLS_ANY ? p.defer[ci] != 0 : p.defer[ci] == CLS; };
   bool any = all;
   for (uint32_t g = blockIdx.x * kWaves + wave; !any && g < ngroups; g += nw) {
     const uint32_t ci = g * 64u + (uint32_t)lane;
-    any = __ballot(ci < nchunks && p.defer[ci] == CLS) != 0;
+    any = __ballot(ci < nchunks && mine(ci)) != 0;
   }
   if (!__syncthreads_or(any)) return;
   // IPv6 Toeplitz table (36 KiB, dynamic LDS: present only with IXG_F_IPV6)
@@ -1102,7 +1110,7 @@ DEV void general_body(const KParams& p) {
     for (int k = 0; k < kQGroups; k++) {
       const uint32_t g = g0 + (uint32_t)k * nw;
       const uint32_t ci = g * 64u + (uint32_t)lane;
-      const bool want = g < ngroups && ci < nchunks && (all || p.defer[ci] == CLS);
+      const bool want = g < ngroups && ci < nchunks && (all || mine(ci));
       const uint64_t m = __ballot(want);
       if (want) q[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
       nq += (uint32_t)__popcll(m);
@@ -1130,6 +1138,10 @@ DEV void general_body(const KParams& p) {
   extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
   NAME(KParams p) { general_body<OFFS, CLS, ##__VA_ARGS__>(p); }
 // variants for A/B (IXGRX_GEN_VARIANT); index 0 is the default
+// behind the coalesced kernel (frames <= 64 B per stride, so deferred
+// chunks are nearly always short): one dispatch takes both classes, saving
+// the empty short dispatch on C2
+IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
 IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2)
 IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
@@ -1253,6 +1265,12 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     // 3x, 4x, 8x and one chunk per wave, which loses the prefetch: -30%)
     const uint32_t gcu = kf == ixg_rx_fastc_s ? 8u * ncu : ncu;
     if (kf) hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, gcu)), dim3(kBlock), 0, (hipStream_t)stream, p);
+  }
+  const bool coal_any = p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0;
+  if (coal_any) {
+    hipLaunchKernelGGL(ixg_rx_any_s, dim3(grid_for(ixg_rx_any_s, group_blocks, ncu, sh6)), dim3(kBlock), sh6,
+                       (hipStream_t)stream, p);
+    return (int)hipGetLastError();
   }
   if (p.defer) {
     const kern_fn ks = k_short[sv][lay];

@@ -257,6 +257,34 @@ def test_fixed_stride_all_fast_and_misaligned_base(engines):
         assert (cs.cpu().numpy().view(np.uint32) == ec).all()
 
 
+def test_small_stride_with_long_lengths(engines):
+    """Fixed stride <= 64 (the coalesced kernel) with some lengths far past
+    the stride: those frames read on into their neighbours' bytes, so their
+    chunks are long-class and take the general kernel's streaming path."""
+    import torch
+    rng = np.random.default_rng(31)
+    n, S = 64 * 300 + 5, 64
+    blob = rng.integers(0, 256, size=n * S + 2048, dtype=np.uint8)
+    base = traces.make_trace("imix", n, seed=32)
+    # real IPv4 headers at every slot start, lengths mostly <= 64, some long
+    for i in range(n):
+        f = base.frame(i)
+        blob[i * S:i * S + min(S, len(f))] = np.frombuffer(f[:S], np.uint8)
+    lens = np.minimum(base.len, 64).astype(np.uint16)
+    longs = rng.random(n) < 0.05
+    lens[longs] = rng.integers(112, 1600, size=int(longs.sum()))
+    tr = traces.Trace(blob, None, lens, S)
+    er, _ = oracle.rx_trace(tr, KEY, threads=8)
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(blob).to(dev)
+    tl = torch.from_numpy(lens.view(np.int16)).to(dev)
+    out = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    engines().batch_dev(tb.data_ptr(), None, tl.data_ptr(), S, n, out.data_ptr(), None,
+                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    _diff(out.cpu().numpy(), er, "stride 64, long lengths")
+
+
 def test_jumbo_frames(engines):
     """Segments far past one streaming round (96 + 2 KiB): jumbo TCP/UDP
     frames of odd and even lengths, some with bad checksums."""
