@@ -445,6 +445,48 @@ def mbuf_path(eng, n: int, seed: int, reps: int = 3):
             "parity": "tiled-consistent" if tiled else "MISMATCH"}, ("mbufs", tr, ptrs, arena, rec)
 
 
+def xgmi_leg(wl, eng, dist, world: int, rank: int, reps: int = 3):
+    """SURVEY 8(e) option 1 (opt-in, N > 1): the whole batch starts in GPU
+    0's HBM (world slices of the workload), one RCCL scatter over xGMI hands
+    every rank its slice, every rank runs the kernels, one RCCL gather brings
+    the 16-byte records back to GPU 0. Phases timed with barriers; the max
+    over ranks of each. Fixed-stride workloads."""
+    import torch
+    from ix_amd import shard
+    assert wl.off is None
+    nbytes = wl.n * wl.stride
+    mine = wl.blob[:nbytes]
+    full = mine.repeat(world) if rank == 0 else None
+    stream = torch.cuda.current_stream()
+    best = None
+    for _ in range(reps):
+        ts = []
+        for phase in range(3):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            if phase == 0:
+                shard.scatter_slices(full, mine, dist)
+            elif phase == 1:
+                wl.launch(eng, stream.cuda_stream)
+            else:
+                back = shard.gather_slices(wl.out, dist)
+            torch.cuda.synchronize()
+            ts.append(shard.max_over_ranks(time.perf_counter() - t0, dist, device="cuda"))
+        best = ts if best is None or sum(ts) < sum(best) else best
+    sc, kr, ga = best
+    ok = True
+    if rank == 0:
+        v = back.view(world, wl.reps, -1, 16)
+        ok = bool(torch.equal(v, v[:1, :1].expand(world, wl.reps, -1, -1)))
+    return {"scatter_ms": round(sc * 1e3, 3), "kernel_ms": round(kr * 1e3, 3), "gather_ms": round(ga * 1e3, 3),
+            "mpps_end_to_end": round(world * wl.n / (sc + kr + ga) / 1e6, 2),
+            "scatter_gbps": round((world - 1) * nbytes / sc / 1e9, 1),
+            "gather_gbps": round((world - 1) * wl.n * 16 / ga / 1e9, 1),
+            "note": "batch in GPU 0's HBM -> RCCL scatter over xGMI -> kernels on every GPU -> RCCL gather of "
+                    "records to GPU 0", "parity": "tiled-consistent" if ok else "MISMATCH"}
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -469,6 +511,7 @@ def main():
     ap.add_argument("--no-copy", action="store_true")
     ap.add_argument("--no-demux", action="store_true")
     ap.add_argument("--no-tx", action="store_true")
+    ap.add_argument("--xgmi", action="store_true", help="N > 1: add the scatter/gather-over-xGMI leg")
     ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
     args = ap.parse_args()
 
@@ -528,6 +571,8 @@ def main():
                      "traffic_source": tsrc},
         "parity": "tiled-consistent" if tiled else "MISMATCH",
     }
+    if args.xgmi and world > 1 and wl.off is None:
+        res["xgmi"] = xgmi_leg(wl, engine(wl.flags), dist, world, rank)
     if args.secondary and args.secondary != args.workload:
         del wl
         torch.cuda.empty_cache()

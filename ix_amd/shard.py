@@ -8,6 +8,10 @@ sizes vary 25x. Each rank copies its own slice host->device (the batch lives
 in host memory, as in IX) and runs ``ixg_rx_batch_*`` on it; nothing crosses
 xGMI on the data path. Records come back in input order through
 ``gather_records``: an all-gather of fixed-size 16-byte records.
+
+When the batch instead starts in one GPU's HBM (SURVEY.md 8(e) option 1),
+``scatter_slices`` / ``gather_slices`` move equal-sized slices out and the
+records back over xGMI with one RCCL scatter and one gather.
 """
 from __future__ import annotations
 
@@ -65,6 +69,35 @@ def gather_records(rec: np.ndarray, bounds: list[tuple[int, int]], dist, device=
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf)
     return np.concatenate([parts[r][:e - s].cpu().numpy() for r, (s, e) in enumerate(bounds)], axis=0)
+
+
+def scatter_slices(full, out, dist, src: int = 0) -> None:
+    """Option 1 of SURVEY.md 8(e): the batch sits on rank `src`'s GPU and its
+    slices travel to the other GPUs over xGMI (one RCCL scatter; torch's
+    backend "nccl" is RCCL on ROCm). `full`: the src rank's flat tensor of
+    world * m elements (None on the other ranks); `out`: every rank's
+    m-element slice. Slices are equal-sized: pad the batch to world * m."""
+    world = dist.get_world_size()
+    if dist.get_rank() == src:
+        if full.numel() != world * out.numel():
+            raise ValueError("full must hold world * out.numel() elements")
+        dist.scatter(out, scatter_list=list(full.view(world, -1).unbind(0)), src=src)
+    else:
+        dist.scatter(out, src=src)
+
+
+def gather_slices(part, dist, dst: int = 0):
+    """The reverse: every rank's equal-sized `part` (e.g. its [m, 16]
+    records) into one [world * m, ...] tensor on rank `dst` (None elsewhere),
+    in rank order, over one RCCL gather."""
+    import torch
+    world = dist.get_world_size()
+    if dist.get_rank() == dst:
+        full = torch.empty((world,) + tuple(part.shape), dtype=part.dtype, device=part.device)
+        dist.gather(part, gather_list=list(full.unbind(0)), dst=dst)
+        return full.view((world * part.shape[0],) + tuple(part.shape[1:]))
+    dist.gather(part, dst=dst)
+    return None
 
 
 def max_over_ranks(x: float, dist, device="cpu") -> float:

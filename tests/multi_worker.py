@@ -37,6 +37,18 @@ def main():
     allrec = shard.gather_records(rec, bounds, dist)
     exp, _ = oracle.rx_trace(tr, traces.RSS_KEY, flags=flags)
     ok = allrec.shape == exp.shape and bool((allrec == exp).all())
+    # option 1: the batch on rank 0, slices scattered, records gathered back
+    import torch
+    m = 4096
+    full = torch.arange(world * m, dtype=torch.int32) if rank == 0 else None
+    mine = torch.empty(m, dtype=torch.int32)
+    shard.scatter_slices(full, mine, dist)
+    ok = ok and bool((mine == torch.arange(rank * m, (rank + 1) * m, dtype=torch.int32)).all())
+    back = shard.gather_slices((mine * 2).view(-1, 4), dist)
+    if rank == 0:
+        ok = ok and bool((back.view(-1) == torch.arange(world * m, dtype=torch.int32) * 2).all())
+    else:
+        ok = ok and back is None
     slowest = shard.max_over_ranks(float(rank + 1), dist)
     ok = ok and slowest == float(world)
     dist.barrier()
