@@ -49,6 +49,10 @@ WORKLOADS = {
     "c4": ("tcp1514", 8 * 1024 * 1024, 1 << 13, "C4 per-GPU shard: 8M x 1514B IPv4/TCP frames (stride 1516)"),
     "c3": ("imix", 16 * 1024 * 1024, 1 << 18, "C3: 16M IMIX 7:4:1 (60/590/1514B) TCP+UDP, packed, u64 offsets"),
     "c5": ("mixed", 16 * 1024 * 1024, 1 << 18, "C5: 16M mixed IPv4 ihl 5..15 + 50% IPv6, packed"),
+    # A/B only (not configs): C5's families alone or in 128-frame runs
+    "c5v4": ("mixed_v4", 16 * 1024 * 1024, 1 << 18, "C5 IPv4 part only (A/B only)"),
+    "c5v6": ("mixed_v6", 16 * 1024 * 1024, 1 << 18, "C5 IPv6 part only (A/B only)"),
+    "c5s": ("mixed_sorted", 16 * 1024 * 1024, 1 << 18, "C5 in 128-frame single-family runs (A/B only)"),
     # A/B only (not a config): C2's frames in the packed u64-offset layout
     "c2o": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2 frames, u64-offset layout (A/B only)"),
 }
@@ -85,7 +89,7 @@ class Workload:
         if name == "c2o":
             tr = self.pool
             self.pool = traces.Trace(tr.blob, tr.offsets().copy(), tr.len, 0)
-        self.flags = 2 if kind == "mixed" else 0
+        self.flags = 2 if kind.startswith("mixed") else 0
         tr = self.pool
         self.bytes_per_pkt = float(alg_bytes(tr).mean())
         self.wire_bytes = float(tr.len.astype(np.int64).mean())

@@ -271,7 +271,10 @@ def make_trace(kind: str, n: int, seed: int, bad_ip: float = 0.0, bad_l4: float 
         size_cls = rng.choice(3, size=n, p=[7 / 12, 4 / 12, 1 / 12])
         proto_cls = rng.integers(0, 2, size=n)
         return pack_classes(classes, (size_cls * 2 + proto_cls).astype(np.int64))
-    if kind == "mixed":
+    if kind in ("mixed", "mixed_v4", "mixed_v6", "mixed_sorted"):
+        # mixed_v4 / mixed_v6: only the IPv4 (ihl 5..15) or only the IPv6
+        # classes; mixed_sorted: C5's mix with each 128-frame run of one
+        # family (A/B of the divergent parse, not a config)
         classes = []
         per = max(1, m // 24)
         for ihl in range(5, 16):
@@ -281,7 +284,10 @@ def make_trace(kind: str, n: int, seed: int, bad_ip: float = 0.0, bad_l4: float 
         for proto in (6, 17):
             classes.append(build_ipv6(rng, per, 94, proto))
         nv4 = 22
-        is6 = rng.random(n) < 0.5
+        p6 = {"mixed": 0.5, "mixed_v4": 0.0, "mixed_v6": 1.0, "mixed_sorted": 0.5}[kind]
+        is6 = rng.random(n) < p6
+        if kind == "mixed_sorted":
+            is6 = (np.arange(n) // 128) % 2 == 1
         cls = np.where(is6, nv4 + rng.integers(0, 2, n), rng.integers(0, nv4, n))
         return pack_classes(classes, cls.astype(np.int64))
     raise ValueError(kind)
