@@ -148,11 +148,16 @@ int ixg_rx_hash_tables(const struct ixg_rx_cfg *cfg, uint64_t *tab, uint32_t *cr
 	return 0;
 }
 
+/* IXG_TAB6_WORDS: for tuple byte i, [2i][n] = the contribution of high
+ * nibble n, [2i+1][n] = that of low nibble n (Toeplitz is linear, so a byte's
+ * contribution is the XOR of its two nibbles') */
 static void hash_table6(const struct ixg_rx_cfg *cfg, uint32_t *tab6)
 {
 	for (int i = 0; i < 36; i++)
-		for (unsigned v = 0; v < 256; v++)
-			tab6[i * 256 + v] = toeplitz_byte(cfg->rss_key, i, v);
+		for (unsigned v = 0; v < 16; v++) {
+			tab6[(2 * i) * 16 + v] = toeplitz_byte(cfg->rss_key, i, v << 4);
+			tab6[(2 * i + 1) * 16 + v] = toeplitz_byte(cfg->rss_key, i, v);
+		}
 }
 
 /* ---- context -------------------------------------------------------------- */
@@ -291,14 +296,14 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 	}
 	free(tab);
 	if (cfg->flags & IXG_F_IPV6) {
-		uint32_t *t6 = (uint32_t *)malloc(36 * 256 * sizeof(uint32_t));
+		uint32_t *t6 = (uint32_t *)malloc(IXG_TAB6_WORDS * sizeof(uint32_t));
 		if (!t6) {
 			rc = -ENOMEM;
 			goto fail;
 		}
 		hash_table6(cfg, t6);
-		if (hipMalloc((void **)&c->d_tab6, 36 * 256 * sizeof(uint32_t)) != hipSuccess ||
-		    hipMemcpy(c->d_tab6, t6, 36 * 256 * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
+		if (hipMalloc((void **)&c->d_tab6, IXG_TAB6_WORDS * sizeof(uint32_t)) != hipSuccess ||
+		    hipMemcpy(c->d_tab6, t6, IXG_TAB6_WORDS * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) {
 			free(t6);
 			goto fail;
 		}

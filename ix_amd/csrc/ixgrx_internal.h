@@ -19,7 +19,7 @@ struct ixg_kparams {
 	struct ixg_rx_rec *out;
 	uint32_t *csum;
 	const uint64_t *tab;   /* 12 x 256: lo = Toeplitz, hi = CRC-32C contribution */
-	const uint32_t *tab6;  /* 36 x 256 Toeplitz contributions (IXG_F_IPV6), or NULL */
+	const uint32_t *tab6;  /* IXG_TAB6_WORDS nibble Toeplitz contributions (IXG_F_IPV6), or NULL */
 	uint32_t stride;
 	uint32_t n;
 	uint32_t crc_const;
@@ -72,6 +72,12 @@ typedef struct ixg_kparams ixg_kparams;
 #define IXG_MODE_SHORT 1u
 #define IXG_MODE_LONG 2u
 #define IXG_MODE_AUTO 0xffffffffu
+
+/* The IPv6-extension Toeplitz table (ixg_kparams.tab6): per input byte of
+ * the 36-byte tuple, 16 entries for its high nibble and 16 for its low one
+ * (72 x 16 u32 = 4.5 KiB), so the general kernels' LDS copy leaves room for
+ * 3 workgroups per CU instead of 2 with a 36 KiB byte table */
+#define IXG_TAB6_WORDS (72u * 16u)
 
 /* implemented in ixgrx_kernels.hip */
 /* enqueue one batch: the fixed-shape kernel (when p->defer) and the general

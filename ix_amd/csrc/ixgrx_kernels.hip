@@ -324,9 +324,15 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   if (v6 && L >= 58 && ver == 6 && (s.proto == 6 || s.proto == 17)) {
     uint32_t h = 0;
 #pragma unroll
-    for (int k = 0; k < 32; k++) h ^= T6[(k << 8) | byte_at(d, 22 + k)];
+    for (int k = 0; k < 32; k++) {
+      const uint32_t b = byte_at(d, 22 + k);
+      h ^= T6[(2 * k) * 16 + (b >> 4)] ^ T6[(2 * k + 1) * 16 + (b & 15u)];
+    }
 #pragma unroll
-    for (int k = 0; k < 4; k++) h ^= T6[((32 + k) << 8) | byte_at(d, 54 + k)];
+    for (int k = 0; k < 4; k++) {
+      const uint32_t b = byte_at(d, 54 + k);
+      h ^= T6[(2 * (32 + k)) * 16 + (b >> 4)] ^ T6[(2 * (32 + k) + 1) * 16 + (b & 15u)];
+    }
     s.rss = h;
     s.flags |= IXG_RF_RSS;
   }
@@ -1092,10 +1098,10 @@ DEV void general_body(const KParams& p) {
     any = __ballot(ci < nchunks && mine(ci)) != 0;
   }
   if (!__syncthreads_or(any)) return;
-  // IPv6 Toeplitz table (36 KiB, dynamic LDS: present only with IXG_F_IPV6)
+  // IPv6 Toeplitz nibble table (4.5 KiB, dynamic LDS: present only with IXG_F_IPV6)
   extern __shared__ u32x4 dyn6[];
   if (p.tab6) {
-    for (int k = threadIdx.x; k < 36 * 256 / 4; k += kBlock) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += kBlock) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
   }
   stage_tables(p, T);
   const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
@@ -1245,7 +1251,7 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   const uint64_t group_blocks = ((nchunks + 63u) / 64u + kWaves - 1) / kWaves; // one wave per 64 chunks
   const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&
                       (reinterpret_cast<uintptr_t>(p.base) & 15u) == 0u;
-  const size_t sh6 = p.tab6 ? 36u * 256u * sizeof(uint32_t) : 0u;
+  const size_t sh6 = p.tab6 ? IXG_TAB6_WORDS * sizeof(uint32_t) : 0u;
   if (p.defer) {
     kern_fn kf = nullptr;
     const bool forced = p.force_mode != IXG_MODE_AUTO;
