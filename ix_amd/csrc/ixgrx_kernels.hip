@@ -590,12 +590,14 @@ struct WaveLds {  // per-wave scratch, LDS address space
   lds_u32* offhi;
   lds_u32* sum;   // per lane: streamed tail sum
   const lds_u32* t6;  // IPv6 Toeplitz table (IXG_F_IPV6), block-shared
+  lds_u32* pre;   // big chunks: the 64 frames' prefixes (kPrefixDw dwords each)
 };
 
 struct Round {
   u32x4 v[kT];
   uint32_t end;   // owner's end of whole pieces (0: this group has no packet)
   uint32_t owner;
+  u32x4 ve;       // big rounds: the piece holding the frame end (group lane 0)
 };
 
 DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, uint32_t nlong, int lane, Round& b) {
@@ -654,6 +656,8 @@ struct GPre {
 };
 
 constexpr uint32_t kNoChunk = 0xffffffffu;
+// big chunks: every frame at least this long (or past the batch end)
+constexpr uint32_t kBigMin = 256;
 
 template <bool OFFS>
 DEV void gen_desc(const KParams& p, uint32_t chunk, int lane, GDesc& g) {
@@ -668,12 +672,141 @@ DEV void gen_desc(const KParams& p, uint32_t chunk, int lane, GDesc& g) {
 // hipcc's vmcnt accounting stays exact across the pipeline
 // GATE: load nothing for a chunk with a frame of IXG_SHORT_MAX bytes or more
 // (the short-first pass leaves such chunks to the long kernel)
-template <bool GATE = false>
+// (a big chunk, see big_chunk, loads its prefixes in its rounds instead)
+template <bool GATE = false, bool BIG = false>
 DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
-  const uint32_t Lg = (!GATE || __all(g.L < IXG_SHORT_MAX)) ? g.L : 0u;
+  const bool skip = GATE ? !__all(g.L < IXG_SHORT_MAX) : (BIG && __all(g.L >= kBigMin || g.L == 0u));
+  const uint32_t Lg = skip ? 0u : g.L;
   load_prefix<0, 6>(p.base + g.off, Lg, reinterpret_cast<const uint8_t*>(p.tab), x.d);
   const bool short_tail = g.L > (uint32_t)kStreamBase && g.L < (uint32_t)kStreamBase + 32u;
   x.v96 = load16(short_tail, p.base + g.off + kStreamBase, p.zero + 16 * lane);
+}
+
+// ---- big chunks ---------------------------------------------------------
+// A chunk whose frames are all >= kBigMin bytes (the 1500 B configs) skips
+// the lane-per-frame prefix pass: 16-lane groups stream every frame from
+// byte 0, 4 frames per round, and the pieces of bytes [0, 96) go to the
+// wave's LDS stash instead of the sum, so each frame's bytes are fetched
+// once, by one group, in one round (a separate prefix pass fetches the lines
+// holding byte 12 and byte 96 a second time, by then evicted from L2: C4's
+// traffic was 1.18x the frame bytes). The streamed sum covers [96, L); the
+// lane then parses its prefix from LDS. A segment ending before L (IPv4
+// ip_len short of the frame) re-sums [96, seg_end) on its own (rare).
+
+DEV void big_issue(const KParams& p, const WaveLds& w, uint32_t r, int lane, Round& b) {
+  const int g = lane / kG, gl = lane % kG;
+  const uint32_t k = r * kRoundPk + (uint32_t)g;
+  const bool act = k < 64u;
+  const uint32_t owner = act ? k : 0u;
+  b.owner = k;
+  b.end = act ? w.end[owner] : 0u;
+  const uint64_t off = ((uint64_t)w.offhi[owner] << 32) | w.offlo[owner];
+  const uint8_t* f = p.base + off;
+  const uint8_t* zero = p.zero + 16 * lane;
+  // whole pieces only; the piece holding L (if L is not a multiple of 16)
+  // is group lane 0's extra load, masked in big_finish
+  const uint32_t whole = b.end & ~15u;
+#pragma unroll
+  for (int t = 0; t < kT; t++) {
+    const uint32_t pos = 16u * gl + 16u * kG * t;
+    b.v[t] = load16(pos < whole, f + pos, zero);
+  }
+  b.ve = load16(gl == 0 && whole < b.end && whole < 16u * kG * kT, f + whole, zero);
+}
+
+DEV u32x4 mask_piece(const u32x4& v, int rem) {
+  return u32x4{v.x & ones(rem < 0 ? 0 : rem), v.y & ones(rem - 4 < 0 ? 0 : rem - 4),
+               v.z & ones(rem - 8 < 0 ? 0 : rem - 8), v.w & ones(rem - 12 < 0 ? 0 : rem - 12)};
+}
+
+DEV void big_finish(const KParams& p, const WaveLds& w, int lane, Round& b) {
+  const int gl = lane % kG;
+  static_assert(kStreamBase == 16 * 6 && kPrefixDw == 24, "the prefix is pieces 0..5 of round slot t = 0");
+  if (gl < 6 && b.owner < 64u) {
+    lds_u32* q = w.pre + b.owner * kPrefixDw + 4 * gl;
+    q[0] = b.v[0].x; q[1] = b.v[0].y; q[2] = b.v[0].z; q[3] = b.v[0].w;
+  }
+  if (gl < 6) b.v[0] = u32x4{0u, 0u, 0u, 0u};
+  uint32_t a = 0, a1 = 0;
+#pragma unroll
+  for (int t = 0; t < kT; t += 4) adc8x2(a, b.v[t], b.v[t + 1], a1, b.v[t + 2], b.v[t + 3]);
+  a = add1c(a, a1);
+  // the end piece (zero page in every other lane): masked to L
+  const u32x4 ve = mask_piece(b.ve, (int)(b.end & 15u));
+  a = add1c(a, fold32((uint64_t)ve.x + ve.y + ve.z + ve.w));
+  // frames longer than 2 KiB (not IX mbufs): the rest, synchronously
+  const uint32_t more = 16u * kG * kT;
+  if (__any(b.end > more)) {
+    const uint32_t owner = b.owner < 64u ? b.owner : 0u;
+    const uint64_t off = ((uint64_t)w.offhi[owner] << 32) | w.offlo[owner];
+    const uint8_t* zero = p.zero + 16 * lane;
+    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 16u * kG) {
+      const uint32_t pos = pos0 + 16u * gl;
+      // (b.ve did not load the end piece of such a frame)
+      const u32x4 v = mask_piece(load16(pos < b.end, p.base + off + pos, zero), (int)b.end - (int)pos);
+      a = add1c(a, fold32((uint64_t)v.x + v.y + v.z + v.w));
+    }
+  }
+#pragma unroll
+  for (int m = 1; m < kG; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, kG));
+  if (gl == 0 && b.owner < 64u) w.sum[b.owner] = a;
+}
+
+// one's complement sum of the frame bytes [a, e) (a 16-aligned), lane-serial
+DEV uint32_t span_sum(const KParams& p, uint64_t off, uint32_t a, uint32_t e) {
+  uint64_t s = 0;
+  for (uint32_t pos = a; pos < e; pos += 16u) {
+    const u32x4 v = mask_piece(load16(true, p.base + off + pos, p.zero), (int)(e - pos));
+    s += (uint64_t)v.x + v.y + v.z + v.w;
+  }
+  return fold32(s);
+}
+
+template <bool OFFS>
+DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, const WaveLds& w,
+                   const GDesc& g) {
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t L = g.L;  // 0 past the end
+  w.end[lane] = L;
+  w.offlo[lane] = (uint32_t)g.off;
+  w.offhi[lane] = (uint32_t)(g.off >> 32);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr uint32_t R = 64 / kRoundPk;
+  Round A, B;
+  big_issue(p, w, 0, lane, A);
+#pragma clang loop unroll(disable)
+  for (uint32_t r = 0; r < R; r += 2) {
+    big_issue(p, w, r + 1, lane, B);
+    big_finish(p, w, lane, A);
+    big_issue(p, w, r + 2, lane, A);
+    big_finish(p, w, lane, B);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  uint32_t d[kPrefixDw];
+  d[0] = d[1] = d[2] = 0;  // MAC addresses: never read
+  const lds_u32* q = w.pre + lane * kPrefixDw;
+#pragma unroll
+  for (int j = 3; j < kPrefixDw; j++) d[j] = q[j];  // L >= 96: no masking
+  LaneState s;
+  const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
+  if (__all(fixed))
+    lane_parse<true, kPrefixDw>(p, T, d, L, s);
+  else
+    lane_parse<false, kPrefixDw>(p, T, d, L, s, w.t6);
+  if (!valid) return;
+  uint32_t res = l4_residual(s);
+  if (s.stream) {
+    const uint32_t tail = s.seg_end == L ? w.sum[lane] : span_sum(p, g.off, (uint32_t)kStreamBase, s.seg_end);
+    res = (~fold16(add1c(fold32(s.l4_acc), tail))) & 0xffffu;
+  }
+  const Rec r = make_record(p, d, L, s, res);
+  store_record(p, i, r, s.ip_res, res);
+  store_demux(p, i, r, s.src, s.dst, s.ports);
 }
 
 // MODE: kModeLong: any chunk; kModeFirst (the short kernel): the chunk's
@@ -682,7 +815,9 @@ DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
 // streaming rounds (compiled out). Returns true when the chunk was deferred.
 constexpr int kModeLong = 0, kModeFirst = 2;
 
-template <bool OFFS, int MODE>
+// BIG: big chunks take big_chunk (the walks without the one-ahead prefix
+// prefetch, so its registers are not live across the rounds)
+template <bool OFFS, int MODE, bool BIG>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x) {
   constexpr bool SHORT = MODE != kModeLong;
@@ -693,6 +828,10 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
     const bool defer = !__all(L < IXG_SHORT_MAX);  // L = 0 past the end
     if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
     if (defer) return true;
+  }
+  if (BIG && __all(g.L >= kBigMin || g.L == 0u)) {
+    big_chunk<OFFS>(p, T, chunk, lane, w, g);
+    return false;
   }
   const uint64_t off = g.off;
   const uint32_t (&d)[kPrefixDw] = x.d;
@@ -1042,20 +1181,21 @@ template <bool OFFS, bool EARLY, int MODE>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
+  constexpr bool BIG = MODE == kModeLong && !EARLY;
   bool deferred = false;
   uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
   GDesc D1;
   gen_desc<OFFS>(p, c1, lane, D1);
   GPre P0;
-  gen_pre<GATE>(p, D0, lane, P0);
+  gen_pre<GATE, BIG>(p, D0, lane, P0);
   for (uint32_t j = 0; j < nq; j++) {
     const uint32_t c2 = j + 2 < nq ? q[j + 2] : kNoChunk;
     GDesc D2;
     gen_desc<OFFS>(p, c2, lane, D2);
     GPre P1;
-    if (EARLY) gen_pre<GATE>(p, D1, lane, P1);
-    deferred |= general_chunk<OFFS, MODE>(p, T, c0, lane, w, D0, P0);
-    if (!EARLY) gen_pre<GATE>(p, D1, lane, P1);
+    if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
+    deferred |= general_chunk<OFFS, MODE, BIG>(p, T, c0, lane, w, D0, P0);
+    if (!EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
     D0 = D1;
@@ -1075,6 +1215,9 @@ DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
       sh_sum[kWaves][64], sh_q[kWaves][64 * kQGroups];
+  // the big-chunk prefix stash (not in the short kernel: no big chunks there)
+  constexpr int kPre = CLS == IXG_CLS_SHORT ? 1 : 64 * kPrefixDw;
+  __shared__ uint32_t sh_pre[kWaves][kPre];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
@@ -1105,7 +1248,8 @@ DEV void general_body(const KParams& p) {
   }
   stage_tables(p, T);
   const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
-                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6)};
+                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6),
+                  LDS(lds_u32, sh_pre[wave])};
   lds_u32* q = LDS(lds_u32, sh_q[wave]);
   bool seen = false;
   // groups g0, g0+nw, ... of this wave, kQGroups at a time: their deferred

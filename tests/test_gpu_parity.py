@@ -303,6 +303,53 @@ def test_jumbo_frames(engines):
         assert (cs == ec).all()
 
 
+def _big_frames(rng, n):
+    """Frames of 256 B or more only, so every chunk takes the long kernel's
+    big-chunk path (prefixes from the streaming rounds): valid IPv4 TCP/UDP
+    with ihl 5..15 and IPv6 of every length class around the 16-byte piece
+    and 2 KiB round boundaries, ICMP echo, fuzzed headers and segments
+    ending before the frame does (ip_len short of L: Ethernet trailer
+    bytes), some with bad checksums."""
+    frames = []
+    for L in (256, 257, 258, 259, 271, 272, 273, 590, 1023, 1514, 2047, 2048, 2049, 2063, 2064, 2065, 2200):
+        for proto in (6, 17):
+            for ihl in (5, 9, 15):
+                rows = traces.build_ipv4(rng, 2, L, proto, ihl=ihl)
+                traces.corrupt(rng, rows, 0.25, 0.25, 14 + 4 * ihl + (16 if proto == 6 else 6))
+                frames += [bytes(r) for r in rows]
+            frames += [bytes(r) for r in traces.build_ipv6(rng, 2, L, proto)]
+    for L in (256, 700, 1514):
+        frames.append(mg.ipv4(proto=1, icmp_type=8, payload=bytes(rng.integers(0, 256, L - 42, dtype=np.uint8))))
+    for f in mg.fuzz_frames(rng, n):
+        f = bytearray(f)
+        if len(f) < 256 or rng.random() < 0.3:
+            # trailer bytes past the IP datagram (or a longer frame around a
+            # truncated one)
+            f += bytes(rng.integers(0, 256, int(rng.integers(256, 1200)), dtype=np.uint8))
+        frames.append(bytes(f))
+    order = rng.permutation(len(frames))
+    return [frames[i] for i in order]
+
+
+def test_big_chunks(engines):
+    rng = np.random.default_rng(0xB16)
+    frames = _big_frames(rng, 6000)
+    assert min(len(f) for f in frames) >= 256
+    tr = traces.pack(frames)
+    for flags in (0, ixgrx.IXG_F_NO_CSUM_DROP, ixgrx.IXG_F_IPV6):
+        rec, cs = engines(flags=flags).batch_trace(tr, want_csum=True)
+        er, ec = oracle.rx_trace(tr, KEY, flags=flags, threads=8)
+        _diff(rec, er, f"big chunks flags={flags}")
+        assert (cs == ec).all()
+    # the same frames at a fixed stride (the stride-layout kernels)
+    S = (max(len(f) for f in frames) + 3) // 4 * 4
+    ts = traces.pack(frames[:3000], stride=S)
+    rec, cs = engines().batch_trace(ts, want_csum=True)
+    er, ec = oracle.rx_trace(ts, KEY, threads=8)
+    _diff(rec, er, "big chunks, stride")
+    assert (cs == ec).all()
+
+
 @pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed"])
 def test_hip_graph_replay(kind):
     """ixg_rx_batch_dev captured once into a HIP graph (torch.cuda.graph) and
