@@ -35,11 +35,12 @@ def kernels(wl) -> str:
     """The dispatches one launch makes (ixgrx_launch): for fixed strides <=
     64 B the coalesced fixed-shape kernel, else the sampler and the lane-load
     one; then the short and the long general kernels (each exits at once
-    when its class has nothing deferred)."""
+    when its class has nothing deferred), or behind the coalesced kernel one
+    general kernel taking both classes (ixg_rx_any_s)."""
     if wl.off is not None:
         return "ixg_rx_sample + ixg_rx_fast_o + ixg_rx_short_o + ixg_rx_general_o"
     if wl.stride <= 64:
-        return "ixg_rx_fastc_s + ixg_rx_short_s + ixg_rx_general_s"
+        return "ixg_rx_fastc_s + ixg_rx_any_s"
     return "ixg_rx_sample + ixg_rx_fast_s + ixg_rx_short_s + ixg_rx_general_s"
 
 

@@ -81,23 +81,66 @@ struct Seg {
   bool valid, udp, full;
 };
 
-// Pass A: lane = segment: descriptor, header dwords, checksum terms.
-DEV Seg tx_prepare(const TParams& p, uint32_t i) {
+// A segment's descriptor (struct ixg_tx_seg, 40 bytes) as loaded
+struct TDesc {
+  u32x4 a, b;
+  uint32_t c;  // ttl | dmac_idx << 16 (rsvd2 is not loaded)
+};
+
+// descriptor loads (segment 0's for lanes past the end: always issued)
+DEV TDesc tx_desc(const TParams& p, uint64_t i) {
+  const uint32_t* dp = reinterpret_cast<const uint32_t*>(p.segs + (i < p.n ? i : 0u));
+  return TDesc{*reinterpret_cast<const u32x4_a4*>(dp), *reinterpret_cast<const u32x4_a4*>(dp + 4), dp[8]};
+}
+
+// the checks of a descriptor and its output pieces K (0 when invalid)
+DEV bool tx_valid(const TParams& p, uint64_t i, const TDesc& d, uint32_t& K) {
+  const uint64_t seg_off = d.a.x | ((uint64_t)d.a.y << 32), out_off = d.a.z | ((uint64_t)d.a.w << 32);
+  const uint32_t seg_len = d.b.z & 0xffffu, proto = (d.b.w >> 16) & 0xffu, dmi = d.c >> 16;
+  const bool tcp = proto == 6u, udp = proto == 17u;
+  const uint32_t l4 = seg_len + (udp ? 8u : 0u);
+  const bool valid = i < p.n && (tcp || udp) && !(tcp && seg_len < 20u) && 20u + l4 <= 0xffffu &&
+                     dmi < p.n_dmac && (seg_off & 3u) == 0u && (out_off & 15u) == 0u;
+  K = valid ? (34u + l4 + 15u) >> 4 : 0u;
+  return valid;
+}
+
+// What pass A needs from memory besides the descriptor: the next-hop MAC
+// and, for a chunk the small path takes, the segment's first 32 bytes.
+// Loaded one chunk ahead (tx_loop), so the descriptor -> data dependency
+// costs no round trip of its own.
+struct TPre {
+  u32x2 dm;
+  u32x4 b0, b1;
+};
+
+DEV void tx_pre(const TParams& p, uint64_t i, const TDesc& d, int lane, TPre& x) {
+  uint32_t K;
+  const bool valid = tx_valid(p, i, d, K);
+  const bool small = __all(K <= 4u);
+  const uint32_t dmi = d.c >> 16;
+  x.dm = *reinterpret_cast<const u32x2*>(p.dmacs + 2u * (valid ? dmi : 0u));
+  const uint64_t sa = reinterpret_cast<uint64_t>(p.seg_buf) + (d.a.x | ((uint64_t)d.a.y << 32));
+  const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
+  const bool ld = small && valid;
+  x.b0 = *reinterpret_cast<const u32x4_a4*>(ld ? sa : zero);
+  x.b1 = *reinterpret_cast<const u32x4_a4*>(ld ? sa + 16u : zero);
+}
+
+// Pass A: lane = segment: header dwords, checksum terms.
+DEV Seg tx_prepare(const TParams& p, uint32_t i, const TDesc& d, const TPre& x) {
   const bool in = i < p.n;
-  const uint32_t* dp = reinterpret_cast<const uint32_t*>(p.segs + (in ? i : 0u));
-  const u32x4 a = *reinterpret_cast<const u32x4_a4*>(dp);
-  const u32x4 b = *reinterpret_cast<const u32x4_a4*>(dp + 4);
-  const u32x2 c = *reinterpret_cast<const u32x2_a4*>(dp + 8);
+  const u32x4 a = d.a, b = d.b;
   const uint64_t seg_off = a.x | ((uint64_t)a.y << 32), out_off = a.z | ((uint64_t)a.w << 32);
   const uint32_t src = b.x, dst = b.y, seg_len = b.z & 0xffffu, sport = b.z >> 16;
   const uint32_t dport = b.w & 0xffffu, proto = (b.w >> 16) & 0xffu, tos = b.w >> 24;
-  const uint32_t ttl = c.x & 0xffu, dmi = c.x >> 16;
+  const uint32_t ttl = d.c & 0xffu;
   const bool tcp = proto == 6u, udp = proto == 17u;
   const uint32_t l4 = seg_len + (udp ? 8u : 0u);
-  const bool valid = in && (tcp || udp) && !(tcp && seg_len < 20u) && 20u + l4 <= 0xffffu && dmi < p.n_dmac &&
-                     (seg_off & 3u) == 0u && (out_off & 15u) == 0u;
+  uint32_t K;
+  const bool valid = tx_valid(p, i, d, K);
   const uint32_t flen = 34u + l4;
-  const u32x2 dm = *reinterpret_cast<const u32x2*>(p.dmacs + 2u * (valid ? dmi : 0u));
+  const u32x2 dm = x.dm;
   const bool offload = (p.flags & IXG_TX_OFFLOAD) != 0u;
   // the header, dwords of frame bytes 0..43 (ip_send_one + tcp_output_packet
   // / ip_setup_header + udp_output)
@@ -132,7 +175,7 @@ DEV Seg tx_prepare(const TParams& p, uint32_t i) {
     // pseudo header as inet_chksum_pseudo_partial adds it (:454-472, :436-437)
     term = (src & 0xffffu) + (src >> 16) + (dst & 0xffffu) + (dst >> 16) + (6u << 8) + bswap16(seg_len);
   }
-  sg.K = valid ? (flen + 15u) >> 4 : 0u;
+  sg.K = K;
   sg.sa = reinterpret_cast<uint64_t>(p.seg_buf) + seg_off;
   sg.oa = reinterpret_cast<uint64_t>(p.out) + out_off;
   sg.seg_len = seg_len;
@@ -259,10 +302,9 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
 // 30 bytes, a UDP payload of at most 22): lane = segment, all in registers.
 // Output pieces 0, 1 are header; piece 2 = header bytes [H-16, H) + body
 // piece 0, piece 3 = body pieces 0 and 1 (as in tx_stream, j = -1 and 0).
-DEV void tx_small(const TParams& p, const Seg& sg, int lane) {
-  const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
-  const u32x4 b0 = *reinterpret_cast<const u32x4_a4*>(sg.valid ? sg.sa : zero);
-  const u32x4 b1 = *reinterpret_cast<const u32x4_a4*>(sg.valid ? sg.sa + 16u : zero);
+// (b0, b1: the segment's first 32 bytes, prefetched by tx_pre; buf: the
+// wave's 4 KiB of LDS for the coalesced store)
+DEV void tx_small(const TParams& p, const Seg& sg, const u32x4& b0, const u32x4& b1, int lane, lds_u32* buf) {
   const uint32_t* h = sg.h;
   u32x4 pm1, o2, o3;
   if (sg.udp) {
@@ -280,6 +322,31 @@ DEV void tx_small(const TParams& p, const Seg& sg, int lane) {
     const uint32_t ck = sg.full ? (~fold16(acc + sg.term)) & 0xffffu : sg.term;
     o3.x = (o3.x & 0xffffu) | (ck << 16);
   }
+  // 64 valid 64-byte frames back to back (packed echo replies): the wave's
+  // 4 KiB go out through LDS as 4 fully coalesced 1 KiB stores instead of
+  // 16-byte pieces into 64 different lines per store
+  const uint64_t oa0 = __shfl(sg.oa, 0);
+  if (__all(sg.valid && sg.K == 4u && sg.oa == oa0 + 64u * (uint32_t)lane)) {
+    lds_u32* q = buf + 16 * lane;
+    const u32x4 pc[4] = {u32x4{h[0], h[1], h[2], h[3]}, u32x4{h[4], h[5], h[6], h[7]}, o2, o3};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      q[4 * k + 0] = pc[k].x; q[4 * k + 1] = pc[k].y; q[4 * k + 2] = pc[k].z; q[4 * k + 3] = pc[k].w;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const lds_u32* r = buf + 4 * (lane + 64 * k);
+      store16(oa0 + 16u * (uint32_t)(lane + 64 * k), u32x4{r[0], r[1], r[2], r[3]});
+    }
+    // the next chunk's LDS writes must not pass these reads
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return;
+  }
   if (sg.valid) {
     store16(sg.oa, u32x4{h[0], h[1], h[2], h[3]});
     store16(sg.oa + 16u, u32x4{h[4], h[5], h[6], h[7]});
@@ -292,30 +359,59 @@ DEV void tx_loop(const TParams& p, const WaveTx& w) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < nchunks; c += nw) {
-    const Seg sg = tx_prepare(p, c * 64u + (uint32_t)lane);
-    const uint32_t K = sg.K;
-    if (__all(K <= 4u)) {
-      tx_small(p, sg, lane);
-      continue;
+  uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (c >= nchunks) return;
+  // software pipeline: descriptors two chunks ahead, MACs and small
+  // segments' bytes one chunk ahead. A chunk the streaming pass takes issues
+  // the next loads only after it, so they do not hold registers across it.
+  TDesc d0 = tx_desc(p, c * 64u + (uint32_t)lane), d1 = tx_desc(p, (c + (uint64_t)nw) * 64u + (uint32_t)lane);
+  TPre x0;
+  tx_pre(p, c * 64u + (uint32_t)lane, d0, lane, x0);
+  for (;; c += nw) {
+    const uint32_t i = c * 64u + (uint32_t)lane;
+    const uint64_t i1 = i + 64ull * nw;
+    const bool last = c + nw >= nchunks;
+    uint32_t K0;
+    tx_valid(p, i, d0, K0);
+    if (__all(K0 <= 4u)) {
+      const TDesc d2 = tx_desc(p, i1 + 64ull * nw);
+      TPre x1;
+      tx_pre(p, i1, d1, lane, x1);
+      const Seg sg = tx_prepare(p, i, d0, x0);
+      tx_small(p, sg, x0.b0, x0.b1, lane, w.src_lo);
+      d0 = d1;
+      d1 = d2;
+      x0 = x1;
+    } else {
+      const Seg sg = tx_prepare(p, i, d0, x0);
+      const uint32_t K = sg.K;
+      tx_publish(sg, lane, w);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (__all(K <= 6u))
+        tx_stream<4>(p, lane, w);
+      else
+        tx_stream<16>(p, lane, w);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const TDesc d2 = tx_desc(p, i1 + 64ull * nw);
+      TPre x1;
+      tx_pre(p, i1, d1, lane, x1);
+      d0 = d1;
+      d1 = d2;
+      x0 = x1;
     }
-    tx_publish(sg, lane, w);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (__all(K <= 6u))
-      tx_stream<4>(p, lane, w);
-    else
-      tx_stream<16>(p, lane, w);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (last) break;
   }
 }
 
 }  // namespace
 
-extern "C" __global__ void __launch_bounds__(kBlock) ixg_tx_build(TParams p) {
+// 4 waves per SIMD: at the 132 VGPRs the pipeline would otherwise take (3
+// waves), mixed-size batches ran 11% slower
+extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) ixg_tx_build(TParams p) {
   __shared__ uint32_t sh[kWaves][(7 + kHdr) * 64];
   lds_u32* b = (lds_u32*)sh[threadIdx.x >> 6];
   const WaveTx w{b, b + 64, b + 128, b + 192, b + 256, b + 320, b + 384, b + 448};
