@@ -1101,6 +1101,49 @@ DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t l
   L = p.len[ic];
 }
 
+// The fused demux of the coalesced kernel, one chunk behind: the chunk's
+// bucket lines are loaded right after its records are stored and matched in
+// the next iteration, after that chunk's frame loads are issued. (Matched at
+// once, the wait for the line -- vmcnt is in order -- also waited for the
+// next chunk's frames, loaded just before: the prefetch became synchronous.)
+struct PendDmx {
+  u32x4 line[4];  // the bucket line (zero page when none)
+  uint32_t i;     // frame index; kNoDmx when the lane stores nothing
+  uint32_t fg, tflags, src, dst, ports;  // fg = kNoDmx: not an IXG_V_TCP record
+};
+constexpr uint32_t kNoDmx = 0xffffffffu;
+
+DEV ixgwalk::Tables dmx_tables(const KParams& p) {
+  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
+}
+
+// record r of frame i (valid lanes) -> pending lookup, line loads issued
+DEV void dmx_issue(const KParams& p, bool valid, uint32_t i, const Rec& r, uint32_t src, uint32_t dst, uint32_t ports,
+                   int lane, PendDmx& q) {
+  const bool tcp = valid && ((r.w0 >> 16) & 0xffu) == IXG_V_TCP;
+  q.i = valid ? i : kNoDmx;
+  q.fg = tcp ? (r.w0 & 0xffffu) - p.fg_base : kNoDmx;
+  q.tflags = (r.w3 >> 16) & 0xffu;
+  q.src = src;
+  q.dst = dst;
+  q.ports = ports;
+  const u32x4* line = tcp ? ixgwalk::bucket_line(dmx_tables(p), q.fg, r.w3 & 0xffffu) : nullptr;
+  const u32x4* src4 = line ? line : reinterpret_cast<const u32x4*>(p.zero + 64 * lane);
+#pragma unroll
+  for (int k = 0; k < 4; k++) q.line[k] = src4[k];
+}
+
+DEV void dmx_finish(const KParams& p, const PendDmx& q) {
+  if (q.i == kNoDmx) return;
+  uint32_t id = 0, kind = IXG_D_NONE;
+  if (q.fg != kNoDmx)
+    ixgwalk::walk_finish(dmx_tables(p), q.fg, q.tflags, q.src, q.dst, q.ports, q.line[0], q.line[1], q.line[2],
+                         q.line[3], id, kind);
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  reinterpret_cast<u32x2v*>(p.dmx)[q.i] = u32x2v{id, kind};
+}
+
+template <bool DMX>
 DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* buf) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
@@ -1112,12 +1155,15 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   const uint32_t fw = (uint32_t)lane * (p.stride >> 2);  // this lane's frame, in dwords
   u32x4 cur[4];
   uint32_t Lc, seen = 0;
+  PendDmx pend;
+  if (DMX) pend.i = kNoDmx;
   fastc_issue(p, c, nchunks, lim, lane, cur, Lc);
   for (;;) {
     const uint32_t cn = c + nw;
     u32x4 nxt[4];
     uint32_t Ln;
     fastc_issue(p, cn, nchunks, lim, lane, nxt, Ln);
+    if (DMX) dmx_finish(p, pend);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       lds_u32* q = buf + 4 * (lane + 64 * k);
@@ -1149,7 +1195,20 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     const uint32_t cls = all_fast ? 0u : defer_class(valid, Lc);
     if (lane == 0) p.defer[c] = (uint8_t)cls;
     seen |= (1u << cls) & ~1u;
-    if (all_fast) process_fast(p, T, i, valid, Lc, d);
+    if (DMX) {
+      // (a deferred chunk's records and demux records are the general kernel's)
+      LaneState s;
+      Rec r{0u, 0u, 0u, 0u};
+      if (all_fast) {
+        lane_parse<true, kFastDw>(p, T, d, Lc, s);
+        const uint32_t r4 = l4_residual(s);
+        r = make_record<true>(p, d, Lc, s, r4);
+        if (valid) store_record<true>(p, i, r, s.ip_res, r4);
+      }
+      dmx_issue(p, all_fast && valid, i, r, s.src, s.dst, s.ports, lane, pend);
+    } else if (all_fast) {
+      process_fast(p, T, i, valid, Lc, d);
+    }
     // the next iteration's LDS writes must not pass this one's reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1160,6 +1219,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     for (int k = 0; k < 4; k++) cur[k] = nxt[k];
     Lc = Ln;
   }
+  if (DMX) dmx_finish(p, pend);
   publish_classes(p, seen, lane);
 }
 
@@ -1168,7 +1228,16 @@ ixg_rx_fastc_s(KParams p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t buf[kWaves][1024];
   stage_tables(p, T);
-  fastc_loop(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
+  fastc_loop<false>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
+}
+
+// with the fused PCB demux (p.dmx set: ixg_rx_demux_batch_dev)
+extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+ixg_rx_fastc_dmx_s(KParams p) {
+  __shared__ uint64_t T[12 * 256];
+  __shared__ uint32_t buf[kWaves][1024];
+  stage_tables(p, T);
+  fastc_loop<true>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
 }
 
 // ---- general kernel --------------------------------------------------------
@@ -1403,7 +1472,7 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
       // coalesced fixed stride: always fixed-shape first (no sampler),
       // unless a test forces another split
       if (forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
-      if (!forced || p.force_mode == IXG_MODE_FAST) kf = ixg_rx_fastc_s;
+      if (!forced || p.force_mode == IXG_MODE_FAST) kf = p.dmx ? ixg_rx_fastc_dmx_s : ixg_rx_fastc_s;
     } else {
       // fast variant 5: no sampler (the fixed-shape kernel always runs first)
       if (fv != 5 || forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
@@ -1413,7 +1482,7 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     // the coalesced kernel runs 8 resident-grids' worth of blocks (each wave
     // ~8 chunks): 3-4% faster on C2 than one persistent grid (A/B of 1x, 2x,
     // 3x, 4x, 8x and one chunk per wave, which loses the prefetch: -30%)
-    const uint32_t gcu = kf == ixg_rx_fastc_s ? 8u * ncu : ncu;
+    const uint32_t gcu = (kf == ixg_rx_fastc_s || kf == ixg_rx_fastc_dmx_s) ? 8u * ncu : ncu;
     if (kf) hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, gcu)), dim3(kBlock), 0, (hipStream_t)stream, p);
   }
   const bool coal_any = p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0;

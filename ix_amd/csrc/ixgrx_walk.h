@@ -41,19 +41,22 @@ __device__ __forceinline__ bool find_list(const ixg_pcb_key* __restrict__ ent, u
   return false;
 }
 
-// The demux record (id | kind << 32 as two dwords) of an IXG_V_TCP frame in
-// local flow group `fg` (fg_id - dev_idx*512), PCB bucket `bucket`
-// (tcp_to_idx), TCP flags `tflags`; src/dst raw (network order as loaded
-// LE), ports host order (sport | dport << 16).
-__device__ __forceinline__ void walk(const Tables& t, uint32_t fg, uint32_t bucket, uint32_t tflags, uint32_t src,
-                                     uint32_t dst, uint32_t ports, uint32_t& id, uint32_t& kind) {
+// The 64-byte bucket line of local flow group `fg`, PCB bucket `bucket`
+// (null when fg is not a group of the tables)
+__device__ __forceinline__ const u32x4* bucket_line(const Tables& t, uint32_t fg, uint32_t bucket) {
+  return fg < t.nfg ? reinterpret_cast<const u32x4*>(t.bline) + 4u * (fg * IXG_PCB_BUCKETS + bucket) : nullptr;
+}
+
+// The lookup given the frame's bucket line (hd, e0..e2; ignored when fg is
+// not a group of the tables): the rest of walk below. Split out so a
+// caller can load the line early and finish later.
+__device__ __forceinline__ void walk_finish(const Tables& t, uint32_t fg, uint32_t tflags, uint32_t src, uint32_t dst,
+                                            uint32_t ports, const u32x4& hd, const u32x4& e0, const u32x4& e1,
+                                            const u32x4& e2, uint32_t& id, uint32_t& kind) {
   bool hit = false;
   id = 0;
   kind = IXG_D_NONE;
   if (fg < t.nfg) {
-    const uint32_t a = fg * IXG_PCB_BUCKETS + bucket;
-    const u32x4* line = reinterpret_cast<const u32x4*>(t.bline) + 4u * a;
-    const u32x4 hd = line[0], e0 = line[1], e1 = line[2], e2 = line[3];
     const uint32_t cnt = hd.x;
     if (cnt > 0u && e0.z == ports && e0.x == src && e0.y == dst) {
       hit = true;
@@ -94,6 +97,23 @@ __device__ __forceinline__ void walk(const Tables& t, uint32_t fg, uint32_t buck
       id = 0;
     }
   }
+}
+
+// The demux record (id | kind << 32 as two dwords) of an IXG_V_TCP frame in
+// local flow group `fg` (fg_id - dev_idx*512), PCB bucket `bucket`
+// (tcp_to_idx), TCP flags `tflags`; src/dst raw (network order as loaded
+// LE), ports host order (sport | dport << 16).
+__device__ __forceinline__ void walk(const Tables& t, uint32_t fg, uint32_t bucket, uint32_t tflags, uint32_t src,
+                                     uint32_t dst, uint32_t ports, uint32_t& id, uint32_t& kind) {
+  const u32x4* line = bucket_line(t, fg, bucket);
+  u32x4 hd = {0u, 0u, 0u, 0u}, e0 = hd, e1 = hd, e2 = hd;
+  if (line) {
+    hd = line[0];
+    e0 = line[1];
+    e1 = line[2];
+    e2 = line[3];
+  }
+  walk_finish(t, fg, tflags, src, dst, ports, hd, e0, e1, e2, id, kind);
 }
 
 }  // namespace ixgwalk
