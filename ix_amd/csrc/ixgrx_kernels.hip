@@ -526,22 +526,39 @@ DEV uint64_t frame_off(const KParams& p, uint32_t i) {
   return OFFS ? p.off[i] : (uint64_t)i * p.stride;
 }
 
-// load 16-byte chunks [K0, K1) of the prefix; chunk k only if 16k < L
+// load 16-byte chunks [K0, K1) of the prefix; chunk k only if 16k < L.
+// Raw: the bytes at offsets >= L are zeroed by mask_prefix where the
+// prefix is consumed (a mask here would make the prefetch wait for its data)
 template <int K0, int K1>
 DEV void load_prefix(const uint8_t* f, uint32_t L, const uint8_t* dummy, uint32_t (&d)[kPrefixDw]) {
   static_assert(K0 == 0, "prefix loads start at the frame start");
   // bytes 0..11 (MAC addresses) are never read: one dword for 12..15
   d[0] = d[1] = d[2] = 0;
-  d[3] = *reinterpret_cast<const uint32_t*>((12u < L ? f : dummy) + 12) & ones((int)L - 12 < 0 ? 0 : (int)L - 12);
+  d[3] = *reinterpret_cast<const uint32_t*>((12u < L ? f : dummy) + 12);
 #pragma unroll
   for (int k = K0 + 1; k < K1; k++) {
     const u32x4 v = load16((uint32_t)(16 * k) < L, f + 16 * k, dummy);
-    // bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L")
-    d[4 * k + 0] = v.x & ones((int)L - (16 * k + 0) < 0 ? 0 : (int)L - (16 * k + 0));
-    d[4 * k + 1] = v.y & ones((int)L - (16 * k + 4) < 0 ? 0 : (int)L - (16 * k + 4));
-    d[4 * k + 2] = v.z & ones((int)L - (16 * k + 8) < 0 ? 0 : (int)L - (16 * k + 8));
-    d[4 * k + 3] = v.w & ones((int)L - (16 * k + 12) < 0 ? 0 : (int)L - (16 * k + 12));
+    d[4 * k + 0] = v.x;
+    d[4 * k + 1] = v.y;
+    d[4 * k + 2] = v.z;
+    d[4 * k + 3] = v.w;
   }
+}
+
+// x & ones(clamp(t, 0, 4)): v_med3 + two shifts (the 64-bit one handles
+// the shift by 32) + v_bfi
+DEV uint32_t keep_bytes(uint32_t x, int t) {
+  const uint32_t u = (uint32_t)(t < 0 ? 0 : (t > 4 ? 4 : t));
+  return x & ~(uint32_t)(~0ull << (8u * u));
+}
+
+// Bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L"). Only the
+// dwords at or past the wave's shortest frame can hold such bytes: the
+// others are left alone (one compare + a wave-uniform branch per dword).
+DEV void mask_prefix(uint32_t (&d)[kPrefixDw], uint32_t L) {
+#pragma unroll
+  for (int j = 3; j < kPrefixDw; j++)
+    if (!__all(L >= 4u * (uint32_t)j + 4u)) d[j] = keep_bytes(d[j], (int)L - 4 * j);
 }
 
 
@@ -834,7 +851,10 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
     return false;
   }
   const uint64_t off = g.off;
-  const uint32_t (&d)[kPrefixDw] = x.d;
+  uint32_t d[kPrefixDw];
+#pragma unroll
+  for (int j = 0; j < kPrefixDw; j++) d[j] = x.d[j];
+  mask_prefix(d, L);
   const u32x4& v96 = x.v96;
   const bool short_tail = L > (uint32_t)kStreamBase && L < (uint32_t)kStreamBase + 32u;
   LaneState s;
