@@ -229,6 +229,15 @@ def parity_leg(checks, key) -> dict:
             _, tr, ptrs, arena, rec = c
             er = oracle.rx_mbufs(key, 128, 0, 0, ptrs[:1 << 16], threads=8, hash_mode=oracle.HASH_TABLE)
             res["mbufs"] = "ok" if np.array_equal(rec.view(np.uint8).reshape(-1, 16)[:1 << 16], er) else "MISMATCH"
+        elif c[0] == "events":
+            _, pool, tabs, pcbs, io, ev0, f0, tiled = c
+            er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
+            dx = oracle.demux_batch(tabs.nfg, tabs.active_start, tabs.active, tabs.tw_start, tabs.tw, tabs.listen,
+                                    0, pool.blob, pool.off, pool.len, pool.stride, er)
+            eev, eidx, _ = oracle.ev_batch(pool.blob, pool.off, 0, er, dx, pcbs, io, 0)
+            ok = ev0 is not None and len(ev0) == len(eev) and \
+                np.array_equal(ev0.view(np.uint8), eev.view(np.uint8)) and np.array_equal(f0, eidx.astype(np.int64))
+            res["events"] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
         elif c[0] == "tx":
             _, kind, (buf, segs, smac, dmacs, out, out_len), tiled = c
             size = int(segs["out_off"][-1]) + 2048
@@ -378,6 +387,91 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
             "separate": {"kernel": "ixg_demux_s over RX records in HBM (ixg_demux_batch_dev)",
                          "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
                          "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4)},
+            "parity": "pending"}, check
+
+
+def events_line(dev, key, steps: int, rank: int, eng_for):
+    """Event records over C3's IMIX shape: 16M frames tiled
+    from 2^16 distinct ones, TCP (with payloads) and UDP half and half, every
+    TCP flow an ESTABLISHED PCB. The RX and demux records come from the fused
+    RX + demux launch (untimed); a step = one ixg_ev_batch_dev launch (count,
+    group, scan, emit): the usys_tcp_recv / usys_udp_recv descriptors, dense and in
+    frame order."""
+    import torch
+    from ix_amd import demux, events, ixgrx
+    wl = Workload("c3", seed=0x1BC000 + 97 * rank, dev=dev, pool=1 << 16)
+    eng = eng_for(0)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    pool, P = wl.pool, wl.pool.n
+    wl.launch(eng, sp)
+    torch.cuda.synchronize()
+    r0 = wl.out[:P].cpu().numpy().reshape(-1).view(ixgrx.REC_DTYPE)
+    tcp = np.nonzero(r0["verdict"] == ixgrx.V["TCP"])[0]
+    keys = demux.tcp_keys(pool.blob, pool.offsets()[tcp])
+    keys["id"] = np.arange(tcp.size, dtype=np.uint32)
+    tabs = demux.DemuxTables.build(eng.cfg, keys, np.zeros(0, demux.PCB_DTYPE), np.zeros(0, demux.LISTEN_DTYPE))
+    demux.load(eng, tabs)
+    n = wl.n
+    rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    dmx = torch.empty((n, 8), dtype=torch.uint8, device=dev)
+    demux.rx_demux_dev(eng, wl.blob.data_ptr(), wl.off.data_ptr(), wl.len.data_ptr(), 0, n, rec.data_ptr(),
+                       dmx.data_ptr(), sp)
+    rng = np.random.default_rng(3)
+    pcbs = np.zeros(tcp.size, dtype=events.PCB_DTYPE)
+    pcbs["pcb_idx"] = rng.integers(0, 1 << 48, size=tcp.size, dtype=np.uint64)
+    pcbs["cookie"] = rng.integers(0, 1 << 63, size=tcp.size, dtype=np.uint64)
+    tp = torch.from_numpy(pcbs.view(np.uint8)).to(dev)
+    ev = torch.empty((n, 40), dtype=torch.uint8, device=dev)
+    fi = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    io = 0x7F0000000000
+
+    def launch():
+        events.batch_dev(eng, wl.blob.data_ptr(), wl.off.data_ptr(), 0, rec.data_ptr(), dmx.data_ptr(), tp.data_ptr(),
+                         tcp.size, n, io, 0, ev.data_ptr(), fi.data_ptr(), cnt.data_ptr(), sp)
+    for _ in range(3):
+        launch()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, c in evs:
+        a.record(stream)
+        launch()
+        c.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = float(np.mean([a.elapsed_time(c) * 1e-3 for a, c in evs]))
+    m = int(cnt.item())
+    # tiling: each repetition's events are the first one's, frame indices
+    # shifted by the pool size and iomap addresses by the repetition's span
+    reps = wl.reps
+    cp = m // reps
+    e = ev[:m].cpu().numpy().reshape(-1).view(events.EV_DTYPE).reshape(reps, cp) if m % reps == 0 else None
+    f = fi[:m].cpu().numpy().astype(np.int64).reshape(reps, cp) if e is not None else None
+    tiled = e is not None
+    if tiled:
+        span = int(wl.off[P].item())
+        sh = (np.arange(reps, dtype=np.uint64) * np.uint64(span))[:, None]
+        udp = e["sysnr"] == events.USYS_UDP_RECV
+        tiled = bool((f - f[:1] == np.arange(reps)[:, None] * P).all()
+                     and (e["sysnr"] == e[:1]["sysnr"]).all() and (e["argb"] == e[:1]["argb"]).all()
+                     and (e["argd"] == e[:1]["argd"]).all()
+                     and (np.where(udp, e["arga"] - sh, e["arga"]) == e[:1]["arga"]).all()
+                     and (e["argc"] - sh == e[:1]["argc"]).all())
+    n_tcp = int((e[0]["sysnr"] == events.USYS_TCP_RECV).sum()) * reps if e is not None else 0
+    # algorithmic bytes: count pass reads the record and demux record (24 B
+    # per frame), emit pass reads them again, then per event the 40-byte
+    # descriptor + 4-byte frame index written, + the 16-byte PCB entry read
+    # for a TCP event
+    alg = 48 * n + 44 * m + 16 * n_tcp
+    check = ("events", pool, tabs, pcbs, io, e[0] if e is not None else None,
+             f[0] if f is not None else None, tiled)
+    return {"workload": "event records over C3's shape: 16M IMIX frames (TCP with payload + UDP), "
+                        f"{tcp.size} established connections; kernels ixg_ev_count + ixg_ev_group + ixg_ev_scan + ixg_ev_emit",
+            "events_per_launch": m, "tcp_events": n_tcp,
+            "mevents_per_s": round(m * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
+            "alg_bytes_per_frame": round(alg / n, 1), "roofline_frac": round(alg / k / 1e9 / PEAK_HBM_GBPS, 4),
             "parity": "pending"}, check
 
 
@@ -599,6 +693,11 @@ def main():
         res["demux"], dchk = demux_line(dev, key, max(5, args.steps // 2), rank, engine)
         checks.append(dchk)
         wl = None
+    if not args.no_demux and args.workload == "c2":
+        torch.cuda.empty_cache()
+        res["events"], echk = events_line(dev, key, max(5, args.steps // 2), rank, engine)
+        checks.append(echk)
+        torch.cuda.empty_cache()
     if not args.no_tx and args.workload == "c2":
         torch.cuda.empty_cache()
         res["tx"] = {}
@@ -635,6 +734,8 @@ def main():
             res["mbuf_path"]["parity"] = par["mbufs"] if res["mbuf_path"]["parity"] != "MISMATCH" else "MISMATCH"
         for kind in res.get("tx", {}):
             res["tx"][kind]["parity"] = par["tx_" + kind]
+        if "events" in res:
+            res["events"]["parity"] = par["events"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -21,7 +21,10 @@ struct ixg_eparams {
 	struct ixg_bsys_desc *ev;
 	uint32_t *frame_idx;
 	uint32_t *count;
-	uint32_t *chunk_base;          /* scratch: per-64-frame chunk event count, then its base */
+	uint32_t *chunk_base;          /* scratch: per-64-frame chunk event count, then its base
+	                                * within its group of 64 chunks */
+	uint32_t *group_base;          /* scratch: per group of 64 chunks, its event count, then
+	                                * its base */
 	uint64_t iomap_base;
 	uint32_t stride;
 	uint32_t n;
@@ -30,7 +33,7 @@ struct ixg_eparams {
 };
 typedef struct ixg_eparams ixg_eparams;
 
-/* implemented in ixgrx_ev.hip: count, scan and emit kernels on `stream` */
+/* implemented in ixgrx_ev.hip: count, group, scan and emit kernels on `stream` */
 int ixgrx_ev_launch(const void *params, uint32_t ncu, void *stream);
 
 #ifdef __cplusplus

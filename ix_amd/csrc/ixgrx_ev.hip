@@ -4,10 +4,14 @@
 // order, so libix's event loop can consume them as they are:
 //   udp_input -> usys_udp_recv  (dp/net/udp.c:81-88, inc/ix/syscall.h:360-365)
 //   recv_a_pbuf -> usys_tcp_recv (dp/net/tcp_api.c:133-147, syscall.h:416-420)
-// Three launches: per 64-frame chunk, count the events (ballot); one block
-// scans the chunk counts into bases (so the output stays in frame order);
-// per chunk, each event lane writes its 40-byte descriptor at base + its
-// rank among the chunk's events (mbcnt).
+// Four launches: per 64-frame chunk, count the events (ballot); per group
+// of 64 chunks, one wave scans the chunk counts (bases within the group and
+// the group's count); one block scans the group counts (so the output stays
+// in frame order); per chunk, the event lanes put their 40-byte descriptors
+// in LDS at their rank among the chunk's events (mbcnt) and the wave stores
+// the chunk's contiguous run of descriptors with coalesced 8-byte stores.
+// (A single block scanning every chunk count took 0.39 ms for 16M frames,
+// stored lane by lane the descriptors 0.26 ms.)
 //
 // No MFMA: a few bytes in, 40 bytes out per event, HBM-bound.
 #include <hip/hip_runtime.h>
@@ -72,15 +76,34 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_count(EParams p) {
   }
 }
 
-// one block: exclusive scan of the chunk counts in place, total to *count
+// one wave per group of 64 chunks: the chunk counts -> bases within the
+// group (exclusive scan), the group's count -> group_base
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_group(EParams p) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nchunks = (p.n + 63u) >> 6, ngroups = (nchunks + 63u) >> 6;
+  const uint32_t g = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (g >= ngroups) return;
+  const uint32_t c = g * 64u + (uint32_t)lane;
+  const uint32_t v = c < nchunks ? p.chunk_base[c] : 0u;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = (uint32_t)__shfl_up((int)incl, d);
+    if (lane >= d) incl += o;
+  }
+  if (c < nchunks) p.chunk_base[c] = incl - v;
+  if (lane == 63) p.group_base[g] = incl;
+}
+
+// one block: exclusive scan of the group counts in place, total to *count
 extern "C" __global__ void __launch_bounds__(1024) ixg_ev_scan(EParams p) {
   __shared__ uint32_t part[1024];
-  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t nchunks = (p.n + 63u) >> 6, ngroups = (nchunks + 63u) >> 6;
   const uint32_t t = threadIdx.x;
-  const uint32_t per = (nchunks + 1023u) / 1024u;
-  const uint32_t b = t * per, e = b + per < nchunks ? b + per : nchunks;
+  const uint32_t per = (ngroups + 1023u) / 1024u;
+  const uint32_t b = t * per, e = b + per < ngroups ? b + per : ngroups;
   uint32_t s = 0;
-  for (uint32_t k = b; k < e; k++) s += p.chunk_base[k];
+  for (uint32_t k = b; k < e; k++) s += p.group_base[k];
   part[t] = s;
   __syncthreads();
   for (uint32_t d = 1; d < 1024u; d <<= 1) {  // Hillis-Steele inclusive scan
@@ -91,14 +114,18 @@ extern "C" __global__ void __launch_bounds__(1024) ixg_ev_scan(EParams p) {
   }
   uint32_t run = part[t] - s;  // exclusive
   for (uint32_t k = b; k < e; k++) {
-    const uint32_t c = p.chunk_base[k];
-    p.chunk_base[k] = run;
+    const uint32_t c = p.group_base[k];
+    p.group_base[k] = run;
     run += c;
   }
   if (t == 1023u) *p.count = part[1023];
 }
 
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+
 extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_emit(EParams p) {
+  __shared__ uint64_t sh[kWaves][64 * 5];
+  lds_u64* buf = (lds_u64*)sh[threadIdx.x >> 6];
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
@@ -106,45 +133,63 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_emit(EParams p) {
     const uint32_t i = c * 64u + (uint32_t)lane;
     const Ev e = classify(p, i);
     const uint64_t m = __ballot(e.on);
-    if (!e.on) continue;
-    const uint32_t slot = p.chunk_base[c] + rank_of(m);
-    const uint64_t foff = p.off ? p.off[i] : (uint64_t)i * p.stride;
-    const uint64_t fio = p.iomap_base + foff;  // iomap(frame start)
-    const uint32_t fg = e.rec.x & 0xffffu, l4_off = e.rec.y & 0xffffu, l4_len = e.rec.y >> 16;
-    ixg_bsys_desc d;
-    if (e.kind) {  // usys_tcp_recv(handle, cookie, iomap(payload), len)
-      const ixg_ev_pcb pc = p.pcbs[e.id];
-      d.sysnr = IXG_USYS_TCP_RECV;
-      d.arga = ((uint64_t)fg << 48) | (pc.pcb_idx & 0xffffffffffffull);
-      d.argb = pc.cookie;
-      d.argc = fio + l4_off;
-      d.argd = l4_len;
-    } else {  // usys_udp_recv(iomap(data), udp->len, iomap(ip_tuple at the frame start))
-      d.sysnr = IXG_USYS_UDP_RECV;
-      d.arga = fio + l4_off;
-      d.argb = l4_len;
-      d.argc = fio;
-      d.argd = 0;
-      if (p.flags & IXG_EV_UDP_TUPLE) {
-        // udp.c:81-86: {ntoh32(src), ntoh32(dst), ntoh16(sport), ntoh16(dport)}
-        uint8_t* f = p.base + foff;
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(f + 24);  // bytes 24..31 (4-aligned)
-        const uint32_t w6 = w[0], w7 = w[1], w8 = w[2];
-        const uint32_t src = (w6 >> 16) | (w7 << 16), dst = (w7 >> 16) | (w8 << 16);  // raw bytes 26..33
-        // the UDP header starts at l4 = l4_off - 8 = 2 mod 4: ports from the
-        // aligned dwords at l4 - 2 and l4 + 2
-        const uint32_t A = *reinterpret_cast<const uint32_t*>(f + l4_off - 10);
-        const uint32_t B = *reinterpret_cast<const uint32_t*>(f + l4_off - 6);
-        const uint32_t sport = (((A >> 16) & 0xffu) << 8) | (A >> 24);
-        const uint32_t dport = ((B & 0xffu) << 8) | ((B >> 8) & 0xffu);
-        uint32_t* o = reinterpret_cast<uint32_t*>(f);
-        o[0] = __builtin_bswap32(src);
-        o[1] = __builtin_bswap32(dst);
-        o[2] = sport | (dport << 16);
+    if (m == 0) continue;
+    const uint32_t base = p.group_base[c >> 6] + p.chunk_base[c], r = rank_of(m);
+    if (e.on) {
+      const uint64_t foff = p.off ? p.off[i] : (uint64_t)i * p.stride;
+      const uint64_t fio = p.iomap_base + foff;  // iomap(frame start)
+      const uint32_t fg = e.rec.x & 0xffffu, l4_off = e.rec.y & 0xffffu, l4_len = e.rec.y >> 16;
+      ixg_bsys_desc d;
+      if (e.kind) {  // usys_tcp_recv(handle, cookie, iomap(payload), len)
+        const ixg_ev_pcb pc = p.pcbs[e.id];
+        d.sysnr = IXG_USYS_TCP_RECV;
+        d.arga = ((uint64_t)fg << 48) | (pc.pcb_idx & 0xffffffffffffull);
+        d.argb = pc.cookie;
+        d.argc = fio + l4_off;
+        d.argd = l4_len;
+      } else {  // usys_udp_recv(iomap(data), udp->len, iomap(ip_tuple at the frame start))
+        d.sysnr = IXG_USYS_UDP_RECV;
+        d.arga = fio + l4_off;
+        d.argb = l4_len;
+        d.argc = fio;
+        d.argd = 0;
+        if (p.flags & IXG_EV_UDP_TUPLE) {
+          // udp.c:81-86: {ntoh32(src), ntoh32(dst), ntoh16(sport), ntoh16(dport)}
+          uint8_t* f = p.base + foff;
+          const uint32_t* w = reinterpret_cast<const uint32_t*>(f + 24);  // bytes 24..31 (4-aligned)
+          const uint32_t w6 = w[0], w7 = w[1], w8 = w[2];
+          const uint32_t src = (w6 >> 16) | (w7 << 16), dst = (w7 >> 16) | (w8 << 16);  // raw bytes 26..33
+          // the UDP header starts at l4 = l4_off - 8 = 2 mod 4: ports from the
+          // aligned dwords at l4 - 2 and l4 + 2
+          const uint32_t A = *reinterpret_cast<const uint32_t*>(f + l4_off - 10);
+          const uint32_t B = *reinterpret_cast<const uint32_t*>(f + l4_off - 6);
+          const uint32_t sport = (((A >> 16) & 0xffu) << 8) | (A >> 24);
+          const uint32_t dport = ((B & 0xffu) << 8) | ((B >> 8) & 0xffu);
+          uint32_t* o = reinterpret_cast<uint32_t*>(f);
+          o[0] = __builtin_bswap32(src);
+          o[1] = __builtin_bswap32(dst);
+          o[2] = sport | (dport << 16);
+        }
       }
+      lds_u64* q = buf + 5 * r;
+      q[0] = d.sysnr;
+      q[1] = d.arga;
+      q[2] = d.argb;
+      q[3] = d.argc;
+      q[4] = d.argd;
+      if (p.frame_idx) p.frame_idx[base + r] = i;
     }
-    p.ev[slot] = d;
-    if (p.frame_idx) p.frame_idx[slot] = i;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the chunk's descriptors are one contiguous run: 8-byte pieces, lane
+    // by lane (5 per descriptor, at most 5 stores per lane)
+    uint64_t* out = reinterpret_cast<uint64_t*>(p.ev + base);
+    const uint32_t nq = 5u * (uint32_t)__popcll(m);
+    for (uint32_t k = (uint32_t)lane; k < nq; k += 64u) out[k] = buf[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 }
 
@@ -157,7 +202,9 @@ extern "C" int ixgrx_ev_launch(const void* params, uint32_t ncu, void* stream) {
   const uint64_t cap = (uint64_t)ncu * (uint64_t)nb;
   const uint32_t grid = (uint32_t)(want < cap ? want : cap);
   hipStream_t s = (hipStream_t)stream;
+  const uint64_t ngroups = (nchunks + 63u) / 64u;
   hipLaunchKernelGGL(ixg_ev_count, dim3(grid ? grid : 1u), dim3(kBlock), 0, s, p);
+  hipLaunchKernelGGL(ixg_ev_group, dim3((uint32_t)((ngroups + kWaves - 1) / kWaves)), dim3(kBlock), 0, s, p);
   hipLaunchKernelGGL(ixg_ev_scan, dim3(1), dim3(1024), 0, s, p);
   hipLaunchKernelGGL(ixg_ev_emit, dim3(grid ? grid : 1u), dim3(kBlock), 0, s, p);
   return (int)hipGetLastError();

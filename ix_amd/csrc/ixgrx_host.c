@@ -914,13 +914,15 @@ int ixg_ev_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ix
 		return -EINVAL;
 	if (n == 0)
 		return hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream) == hipSuccess ? 0 : -EIO;
-	size_t nchunks = ((size_t)n + 63) / 64;
-	if (nchunks > c->evbase_cap) {
+	/* scratch: chunk counts/bases, then group counts/bases (64 chunks a group) */
+	size_t nchunks = ((size_t)n + 63) / 64, ngroups = (nchunks + 63) / 64;
+	size_t need = ngroups * 64 + ngroups;
+	if (need > c->evbase_cap) {
 		hipFree(c->d_evbase);
 		c->d_evbase = NULL;
 		c->evbase_cap = 0;
-		HIPCHK(hipMalloc((void **)&c->d_evbase, nchunks * sizeof(uint32_t)));
-		c->evbase_cap = nchunks;
+		HIPCHK(hipMalloc((void **)&c->d_evbase, need * sizeof(uint32_t)));
+		c->evbase_cap = need;
 	}
 	struct ixg_eparams p;
 	memset(&p, 0, sizeof(p));
@@ -933,6 +935,7 @@ int ixg_ev_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ix
 	p.frame_idx = d_frame_idx;
 	p.count = d_count;
 	p.chunk_base = c->d_evbase;
+	p.group_base = c->d_evbase + ngroups * 64;
 	p.iomap_base = iomap_base;
 	p.stride = fr->stride;
 	p.n = n;
