@@ -54,6 +54,8 @@ WORKLOADS = {
     "c5v4": ("mixed_v4", 16 * 1024 * 1024, 1 << 18, "C5 IPv4 part only (A/B only)"),
     "c5v6": ("mixed_v6", 16 * 1024 * 1024, 1 << 18, "C5 IPv6 part only (A/B only)"),
     "c5s": ("mixed_sorted", 16 * 1024 * 1024, 1 << 18, "C5 in 128-frame single-family runs (A/B only)"),
+    # C2 with 1% bad IP and 1% bad TCP checksums (flag paths)
+    "c2b": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2 with 1% bad IP + 1% bad TCP checksums (L=60, stride 60)"),
     # A/B only (not a config): C2's frames in the packed u64-offset layout
     "c2o": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2 frames, u64-offset layout (A/B only)"),
 }
@@ -86,7 +88,8 @@ class Workload:
         pool = min(pool or pool_def, self.n)
         assert self.n % pool == 0
         self.reps = self.n // pool
-        self.pool = traces.make_trace(kind, pool, seed=seed)
+        bad = 0.01 if name == "c2b" else 0.0
+        self.pool = traces.make_trace(kind, pool, seed=seed, bad_ip=bad, bad_l4=bad)
         if name == "c2o":
             tr = self.pool
             self.pool = traces.Trace(tr.blob, tr.offsets().copy(), tr.len, 0)
@@ -152,7 +155,7 @@ def time_steps(wl, eng, steps, warmup, dist, world):
     kern = [a.elapsed_time(b) * 1e-3 for a, b in ev]
     if world > 1:
         from ix_amd.shard import max_over_ranks
-        el = max_over_ranks(el, dist, device="cuda")
+        el = max_over_ranks(el, dist, device="cuda" if dist.get_backend() == "nccl" else "cpu")
     return el, float(np.mean(kern)), float(np.min(kern))
 
 
@@ -387,7 +390,7 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
             "separate": {"kernel": "ixg_demux_s over RX records in HBM (ixg_demux_batch_dev)",
                          "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
                          "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4)},
-            "parity": "pending"}, check
+            "parity": "tiled-consistent" if check[-1] else "MISMATCH"}, check
 
 
 def events_line(dev, key, steps: int, rank: int, eng_for):
@@ -472,7 +475,7 @@ def events_line(dev, key, steps: int, rank: int, eng_for):
             "events_per_launch": m, "tcp_events": n_tcp,
             "mevents_per_s": round(m * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
             "alg_bytes_per_frame": round(alg / n, 1), "roofline_frac": round(alg / k / 1e9 / PEAK_HBM_GBPS, 4),
-            "parity": "pending"}, check
+            "parity": "tiled-consistent" if check[-1] else "MISMATCH"}, check
 
 
 def tx_line(dev, steps: int, eng, kind: str, n: int):
@@ -610,6 +613,7 @@ def main():
     ap.add_argument("--no-copy", action="store_true")
     ap.add_argument("--no-demux", action="store_true")
     ap.add_argument("--no-tx", action="store_true")
+    ap.add_argument("--no-bad", action="store_true", help="skip the C2 bad-checksum line")
     ap.add_argument("--xgmi", action="store_true", help="N > 1: add the scatter/gather-over-xGMI leg")
     ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
     args = ap.parse_args()
@@ -621,11 +625,19 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # IXG_BENCH_BACKEND=gloo (with ranks sharing a card: device = LOCAL_RANK
+    # mod the device count) rehearses the N > 1 path on a one-GPU box; the
+    # driver's multi-GPU runs use the default, nccl (RCCL), one rank per GPU
+    backend = os.environ.get("IXG_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     key = traces.RSS_KEY
     engs = {}
 
@@ -670,6 +682,24 @@ def main():
                      "traffic_source": tsrc},
         "parity": "tiled-consistent" if tiled else "MISMATCH",
     }
+    if args.workload == "c2" and not args.no_bad:
+        # the same shape with checksum failures: the verdict/flag paths of
+        # the fixed-shape kernel (a bad frame stays on the fast path)
+        del wl
+        torch.cuda.empty_cache()
+        wlb = Workload("c2b", seed=0x1B0000 + 2 + 0x100 + 97 * rank, dev=dev)
+        kb = max(5, args.steps // 2)
+        elb, kbavg, _ = time_steps(wlb, engine(wlb.flags), kb, 2, dist, world)
+        tb, fb = wlb.snapshot()
+        checks.append(("rx", wlb.name, wlb.pool, wlb.flags, fb, tb))
+        vb = np.ascontiguousarray(fb).view(ixgrx.REC_DTYPE).reshape(-1)["verdict"]
+        res["bad_csum"] = {"workload": wlb.desc, "mpps": round(wlb.n * kb * world / elb / 1e6, 2),
+                           "kernel_ms_avg": round(kbavg * 1e3, 4),
+                           "roofline_frac": round(wlb.bytes_per_pkt * wlb.n / kbavg / 1e9 / PEAK_HBM_GBPS, 4),
+                           "verdicts_per_pool": {ixgrx.VERDICTS[int(v)]: int(c) for v, c in
+                                                 zip(*np.unique(vb, return_counts=True))},
+                           "parity": "tiled-consistent" if tb else "MISMATCH"}
+        wl = wlb
     if args.xgmi and world > 1 and wl.off is None:
         res["xgmi"] = xgmi_leg(wl, engine(wl.flags), dist, world, rank)
     if args.secondary and args.secondary != args.workload:
@@ -736,6 +766,8 @@ def main():
             res["tx"][kind]["parity"] = par["tx_" + kind]
         if "events" in res:
             res["events"]["parity"] = par["events"]
+        if "bad_csum" in res:
+            res["bad_csum"]["parity"] = par["c2b"]
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
