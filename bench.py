@@ -56,6 +56,8 @@ WORKLOADS = {
     "c5s": ("mixed_sorted", 16 * 1024 * 1024, 1 << 18, "C5 in 128-frame single-family runs (A/B only)"),
     # C2 with 1% bad IP and 1% bad TCP checksums (flag paths)
     "c2b": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2 with 1% bad IP + 1% bad TCP checksums (L=60, stride 60)"),
+    # A/B only (not a config): C2's slots, IPv4 with one option word (all deferred)
+    "c2opt": ("tcp64opt", 16 * 1024 * 1024, 1 << 20, "C2 slots, IPv4 ihl 6 (A/B only)"),
     # A/B only (not a config): C2's frames in the packed u64-offset layout
     "c2o": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2 frames, u64-offset layout (A/B only)"),
 }

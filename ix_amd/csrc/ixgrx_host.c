@@ -273,6 +273,8 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		c->fast_variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
 		e = getenv("IXGRX_SHORT_VARIANT");
 		c->fast_variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
+		e = getenv("IXGRX_ANY_VARIANT");
+		c->fast_variant |= e ? ((atoi(e) & 0x7f) << 24) : 0;
 		e = getenv("IXGRX_MODE");
 		c->force_mode = IXG_MODE_AUTO;
 		if (e && !strcmp(e, "fast"))

@@ -1475,7 +1475,7 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
 // 0's lane-load kernel.
 extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
-  int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff;
+  int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff, av = (variant >> 24) & 0x7f;
   if (gv >= k_ngen) gv = 0;
   if (sv >= k_nshort) sv = 0;
   const int lay = p.off ? 1 : 0;
@@ -1507,7 +1507,10 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   }
   const bool coal_any = p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0;
   if (coal_any) {
-    hipLaunchKernelGGL(ixg_rx_any_s, dim3(grid_for(ixg_rx_any_s, group_blocks, ncu, sh6)), dim3(kBlock), sh6,
+    // any variant k > 0 (A/B): at most ncu / k blocks
+    const uint32_t acu = av ? (ncu / (uint32_t)av ? ncu / (uint32_t)av : 1u) : ncu;
+    hipLaunchKernelGGL(ixg_rx_any_s, dim3(av ? (group_blocks < acu ? (uint32_t)group_blocks : acu)
+                                             : grid_for(ixg_rx_any_s, group_blocks, ncu, sh6)), dim3(kBlock), sh6,
                        (hipStream_t)stream, p);
     return (int)hipGetLastError();
   }

@@ -253,6 +253,13 @@ def make_trace(kind: str, n: int, seed: int, bad_ip: float = 0.0, bad_l4: float 
         if m < n:
             rows = rows[np.arange(n) % m]
         return pack_rows(rows, 60)
+    if kind == "tcp64opt":
+        # C2's slots with one option word (ihl 6): every chunk leaves the
+        # fixed-shape path (A/B of the deferred path, not a config)
+        rows = build_ipv4(rng, m, 60, 6, ihl=6)
+        if m < n:
+            rows = rows[np.arange(n) % m]
+        return pack_rows(rows, 60)
     if kind == "tcp1514":
         rows = build_ipv4(rng, m, 1514, 6)
         corrupt(rng, rows, bad_ip, bad_l4, 34 + 16)

@@ -38,6 +38,7 @@ def main():
         os.environ["IXGRX_FAST_VARIANT"] = parts[0] or "0"
         os.environ["IXGRX_GEN_VARIANT"] = parts[1] or "0"
         os.environ["IXGRX_SHORT_VARIANT"] = parts[2] or "0"
+        os.environ["IXGRX_ANY_VARIANT"] = (parts[3] if len(parts) > 3 else "0") or "0"
         engs[v] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags))
     s = torch.cuda.current_stream()
     times = {v: [] for v in engs}
