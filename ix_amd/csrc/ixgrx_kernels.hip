@@ -614,15 +614,34 @@ struct Round {
   u32x4 v[kT];
   uint32_t end;   // owner's end of whole pieces (0: this group has no packet)
   uint32_t owner;
+  uint32_t gsh;   // general rounds: log2 of the group size
   u32x4 ve;       // big rounds: the piece holding the frame end (group lane 0)
 };
 
-DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, uint32_t nlong, int lane, Round& b) {
-  const int g = lane / kG, gl = lane % kG;
-  const uint32_t k = r * kRoundPk + (uint32_t)g;
-  const bool act = k < nlong;
+// Which list entry a round's group streams. With the medium split
+// (RoundPlan.rm > 0), rounds [0, rm) take the medium segments (whole
+// pieces ending at or below kStreamBase + kMedSpan) with 4-lane groups, 16
+// segments per round, 512 B each; the rounds after take the rest with
+// 16-lane groups, 4 per round, 2 KiB each. (16-lane groups alone: a 590-B
+// frame's 31 pieces used 31 of a group's 128 load slots.)
+constexpr uint32_t kMedG = 4;
+constexpr uint32_t kMedSpan = 16u * kMedG * kT;  // 512
+struct RoundPlan {
+  uint32_t nmed;   // list entries [0, nmed): medium segments
+  uint32_t nlong;  // list entries [0, nlong): every long segment
+  uint32_t rm;     // rounds of medium segments (0: no split)
+};
+
+template <bool MED>
+DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, const RoundPlan& plan, int lane, Round& b) {
+  const bool med = MED && r < plan.rm;  // wave-uniform
+  const uint32_t gsh = med ? 2u : 4u;  // log2 of the group size
+  const uint32_t g = (uint32_t)lane >> gsh, gl = (uint32_t)lane & ((1u << gsh) - 1u);
+  const uint32_t k = med ? r * (64u >> gsh) + g : plan.nmed + (r - plan.rm) * (uint32_t)kRoundPk + g;
+  const bool act = k < (med ? plan.nmed : plan.nlong);
   const uint32_t owner = w.list[act ? k : 0u];
   b.owner = owner;
+  b.gsh = gsh;
   b.end = act ? w.end[owner] : 0u;
   const uint64_t off = ((uint64_t)w.offhi[owner] << 32) | w.offlo[owner];
   const uint8_t* f = p.base + off;
@@ -630,13 +649,16 @@ DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, uint32_t nl
   const uint8_t* zero = p.zero + 16 * lane;
 #pragma unroll
   for (int t = 0; t < kT; t++) {
-    const uint32_t pos = kStreamBase + 16u * gl + 16u * kG * t;
+    const uint32_t pos = kStreamBase + 16u * gl + (16u << gsh) * (uint32_t)t;
     b.v[t] = load16(pos < b.end, f + pos, zero);
   }
 }
 
+template <bool MED>
 DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round& b) {
-  const int gl = lane % kG;
+  const uint32_t gsh = MED ? b.gsh : 4u;
+  const uint32_t gsz = 1u << gsh;
+  const uint32_t gl = (uint32_t)lane & (gsz - 1u);
   // every piece is inside the segment or reads the zero page (pass A summed
   // the piece holding the segment end, masked): plain one's complement sums
   static_assert(kT % 4 == 0, "two interleaved chains of piece pairs");
@@ -645,19 +667,21 @@ DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round&
   for (int t = 0; t < kT; t += 4) adc8x2(a, b.v[t], b.v[t + 1], a1, b.v[t + 2], b.v[t + 3]);
   a = add1c(a, a1);
   // frames longer than 96 + 2 KiB (not IX mbufs): the rest, synchronously
-  const uint32_t more = kStreamBase + 16u * kG * kT;
+  const uint32_t more = kStreamBase + (16u << gsh) * kT;
   if (__any(b.end > more)) {
     const uint64_t off = ((uint64_t)w.offhi[b.owner] << 32) | w.offlo[b.owner];
     const uint8_t* zero = p.zero + 16 * lane;
-    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 32u * kG) {
+    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 32u * gsz) {
       const uint32_t pos = pos0 + 16u * gl;
       const u32x4 v0 = load16(pos < b.end, p.base + off + pos, zero);
-      const u32x4 v1 = load16(pos + 16u * kG < b.end, p.base + off + pos + 16u * kG, zero);
+      const u32x4 v1 = load16(pos + 16u * gsz < b.end, p.base + off + pos + 16u * gsz, zero);
       a = adc8(a, v0, v1);
     }
   }
+  // group reduction (xor partners below the group size stay in the group)
 #pragma unroll
-  for (int m = 1; m < kG; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, kG));
+  for (uint32_t m = 1; m < (uint32_t)kG; m <<= 1)
+    if (m < gsz) a = add1c(a, (uint32_t)__shfl_xor((int)a, (int)m));
   if (gl == 0 && b.end != 0u) w.sum[b.owner] = a;
 }
 
@@ -834,7 +858,7 @@ constexpr int kModeLong = 0, kModeFirst = 2;
 
 // BIG: big chunks take big_chunk (the walks without the one-ahead prefix
 // prefetch, so its registers are not live across the rounds)
-template <bool OFFS, int MODE, bool BIG>
+template <bool OFFS, int MODE, bool BIG, bool MED = false>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x) {
   constexpr bool SHORT = MODE != kModeLong;
@@ -897,23 +921,31 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   asm volatile("" : "+v"(rbad.w0), "+v"(rbad.w1), "+v"(rbad.w2), "+v"(rbad.w3));
   asm volatile("" : "+v"(acc32), "+v"(ip_res));
   asm volatile("" : "+v"(tsrc), "+v"(tdst), "+v"(tports));
+  // MED: the medium segments first in the list (4-lane groups), then the rest
+  const bool lmed = MED && lng && pend <= (uint32_t)kStreamBase + kMedSpan;
+  const uint64_t mm = MED ? __ballot(lmed) : 0ull, mb = MED ? m & ~mm : m;
+  const uint32_t nmed = (uint32_t)__popcll(mm);
   if (lng) {
-    w.list[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = (uint32_t)lane;
+    const uint64_t mine = lmed ? mm : mb;
+    const uint32_t at = (lmed ? 0u : nmed) +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    w.list[at] = (uint32_t)lane;
     w.end[lane] = pend;
     w.offlo[lane] = (uint32_t)off;
     w.offhi[lane] = (uint32_t)(off >> 32);
   }
   __builtin_amdgcn_wave_barrier();
   const uint32_t nlong = (uint32_t)__popcll(m);
-  const uint32_t R = (nlong + kRoundPk - 1) / kRoundPk;
+  const RoundPlan plan{nmed, nlong, MED ? (nmed + 64u / kMedG - 1u) / (64u / kMedG) : 0u};
+  const uint32_t R = plan.rm + (nlong - nmed + kRoundPk - 1) / kRoundPk;
   Round A, B;
-  round_issue(p, w, 0, nlong, lane, A);
+  round_issue<MED>(p, w, 0, plan, lane, A);
 #pragma clang loop unroll(disable)
   for (uint32_t r = 0; r < R; r += 2) {
-    round_issue(p, w, r + 1, nlong, lane, B);
-    round_finish(p, w, lane, A);
-    round_issue(p, w, r + 2, nlong, lane, A);
-    round_finish(p, w, lane, B);
+    round_issue<MED>(p, w, r + 1, plan, lane, B);
+    round_finish<MED>(p, w, lane, A);
+    round_issue<MED>(p, w, r + 2, plan, lane, A);
+    round_finish<MED>(p, w, lane, B);
   }
   __builtin_amdgcn_wave_barrier();
   if (valid) {
@@ -1266,7 +1298,7 @@ ixg_rx_fastc_dmx_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, int MODE>
+template <bool OFFS, bool EARLY, int MODE, bool MED = false>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
@@ -1283,7 +1315,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     gen_desc<OFFS>(p, c2, lane, D2);
     GPre P1;
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
-    deferred |= general_chunk<OFFS, MODE, BIG>(p, T, c0, lane, w, D0, P0);
+    deferred |= general_chunk<OFFS, MODE, BIG, MED>(p, T, c0, lane, w, D0, P0);
     if (!EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
@@ -1299,7 +1331,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // fixed-shape kernel deferred as short or, in IXG_MODE_SHORT, walks every
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
-template <bool OFFS, uint32_t CLS, bool SEARLY = true>
+template <bool OFFS, uint32_t CLS, bool SEARLY = true, bool MED = false>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -1365,9 +1397,9 @@ DEV void general_body(const KParams& p) {
     if (CLS == IXG_CLS_SHORT)
       seen |= gen_walk<OFFS, SEARLY, kModeFirst>(p, T, w, q, nq, lane, D0);
     else if (__any(D0.L > (uint32_t)kStreamBase + 32u))
-      gen_walk<OFFS, false, kModeLong>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, false, kModeLong, MED>(p, T, w, q, nq, lane, D0);
     else
-      gen_walk<OFFS, true, kModeLong>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, true, kModeLong, MED>(p, T, w, q, nq, lane, D0);
     __builtin_amdgcn_wave_barrier();
   }
   if (CLS == IXG_CLS_SHORT) publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
@@ -1381,12 +1413,16 @@ DEV void general_body(const KParams& p) {
 // chunks are nearly always short): one dispatch takes both classes, saving
 // the empty short dispatch on C2
 IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
-IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2)
-IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2)
+// (the default streams medium segments with 4-lane groups: C3 -5.5% in A/B)
+IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, true)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, true)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
 IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, IXG_CLS_LONG, 4)
+// every long segment streamed by 16-lane groups (the split's A/B baseline)
+IXG_GEN_KERNEL(ixg_rx_general_g16_s, false, IXG_CLS_LONG, 2)
+IXG_GEN_KERNEL(ixg_rx_general_g16_o, true, IXG_CLS_LONG, 2)
 // the short-class general kernel (no streaming rounds); variants for A/B
 // (IXGRX_SHORT_VARIANT), index 0 the default
 IXG_GEN_KERNEL(ixg_rx_short_s, false, IXG_CLS_SHORT, 3)
@@ -1436,7 +1472,8 @@ static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
                                     {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}};
 static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
                                    {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
-                                   {ixg_rx_general_w4_s, ixg_rx_general_w4_o}};
+                                   {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
+                                   {ixg_rx_general_g16_s, ixg_rx_general_g16_o}};
 static const kern_fn k_short[][2] = {{ixg_rx_short_s, ixg_rx_short_o},
                                      {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
                                      {ixg_rx_short_late_s, ixg_rx_short_late_o}};
