@@ -618,27 +618,42 @@ struct Round {
   u32x4 ve;       // big rounds: the piece holding the frame end (group lane 0)
 };
 
-// Which list entry a round's group streams. With the medium split
-// (RoundPlan.rm > 0), rounds [0, rm) take the medium segments (whole
-// pieces ending at or below kStreamBase + kMedSpan) with 4-lane groups, 16
-// segments per round, 512 B each; the rounds after take the rest with
-// 16-lane groups, 4 per round, 2 KiB each. (16-lane groups alone: a 590-B
-// frame's 31 pieces used 31 of a group's 128 load slots.)
+// Which list entry a round's group streams (SM, the stream mapping):
+// 0: every long segment by a 16-lane group, 4 per round, 2 KiB each.
+// 1: rounds [0, rm) take the medium segments (whole pieces ending at or
+//    below kStreamBase + kMedSpan) by 4-lane groups, 16 per round, 512 B
+//    each; the rounds after take the rest as in 0.
+// 2: packed: the list (medium entries first) laid out over consecutive
+//    lanes, 4 per medium entry and 16 per other entry (the first of those
+//    16-aligned), 64 lanes per round; tail rounds of the two kinds share.
+// (16-lane groups alone: a 590-B frame's 31 pieces used 31 of a group's 128
+// load slots.)
 constexpr uint32_t kMedG = 4;
 constexpr uint32_t kMedSpan = 16u * kMedG * kT;  // 512
 struct RoundPlan {
   uint32_t nmed;   // list entries [0, nmed): medium segments
   uint32_t nlong;  // list entries [0, nlong): every long segment
-  uint32_t rm;     // rounds of medium segments (0: no split)
+  uint32_t rm;     // SM 1: rounds of medium segments
 };
 
-template <bool MED>
+template <int SM>
 DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, const RoundPlan& plan, int lane, Round& b) {
-  const bool med = MED && r < plan.rm;  // wave-uniform
-  const uint32_t gsh = med ? 2u : 4u;  // log2 of the group size
-  const uint32_t g = (uint32_t)lane >> gsh, gl = (uint32_t)lane & ((1u << gsh) - 1u);
-  const uint32_t k = med ? r * (64u >> gsh) + g : plan.nmed + (r - plan.rm) * (uint32_t)kRoundPk + g;
-  const bool act = k < (med ? plan.nmed : plan.nlong);
+  uint32_t gsh, k;
+  bool act;
+  if (SM == 2) {
+    const uint32_t G = 64u * r + (uint32_t)lane, bigb = 4u * ((plan.nmed + 3u) & ~3u);
+    const bool big = G >= bigb;
+    gsh = big ? 4u : 2u;
+    k = big ? plan.nmed + ((G - bigb) >> 4) : G >> 2;
+    act = big ? k < plan.nlong : k < plan.nmed;
+  } else {
+    const bool med = SM == 1 && r < plan.rm;  // wave-uniform
+    gsh = med ? 2u : 4u;
+    const uint32_t g = (uint32_t)lane >> gsh;
+    k = med ? r * (64u >> gsh) + g : plan.nmed + (r - plan.rm) * (uint32_t)kRoundPk + g;
+    act = k < (med ? plan.nmed : plan.nlong);
+  }
+  const uint32_t gl = (uint32_t)lane & ((1u << gsh) - 1u);
   const uint32_t owner = w.list[act ? k : 0u];
   b.owner = owner;
   b.gsh = gsh;
@@ -654,9 +669,9 @@ DEV void round_issue(const KParams& p, const WaveLds& w, uint32_t r, const Round
   }
 }
 
-template <bool MED>
+template <int SM>
 DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round& b) {
-  const uint32_t gsh = MED ? b.gsh : 4u;
+  const uint32_t gsh = SM ? b.gsh : 4u;
   const uint32_t gsz = 1u << gsh;
   const uint32_t gl = (uint32_t)lane & (gsz - 1u);
   // every piece is inside the segment or reads the zero page (pass A summed
@@ -678,10 +693,13 @@ DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round&
       a = adc8(a, v0, v1);
     }
   }
-  // group reduction (xor partners below the group size stay in the group)
+  // group reduction: every lane shuffles (SM 2 mixes group sizes in a
+  // wave); xor partners below a lane's group size stay in its group
 #pragma unroll
-  for (uint32_t m = 1; m < (uint32_t)kG; m <<= 1)
-    if (m < gsz) a = add1c(a, (uint32_t)__shfl_xor((int)a, (int)m));
+  for (uint32_t m = 1; m < (uint32_t)kG; m <<= 1) {
+    const uint32_t x = (uint32_t)__shfl_xor((int)a, (int)m);
+    if (m < gsz) a = add1c(a, x);
+  }
   if (gl == 0 && b.end != 0u) w.sum[b.owner] = a;
 }
 
@@ -858,7 +876,7 @@ constexpr int kModeLong = 0, kModeFirst = 2;
 
 // BIG: big chunks take big_chunk (the walks without the one-ahead prefix
 // prefetch, so its registers are not live across the rounds)
-template <bool OFFS, int MODE, bool BIG, bool MED = false>
+template <bool OFFS, int MODE, bool BIG, int SM = 0>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x) {
   constexpr bool SHORT = MODE != kModeLong;
@@ -921,7 +939,8 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   asm volatile("" : "+v"(rbad.w0), "+v"(rbad.w1), "+v"(rbad.w2), "+v"(rbad.w3));
   asm volatile("" : "+v"(acc32), "+v"(ip_res));
   asm volatile("" : "+v"(tsrc), "+v"(tdst), "+v"(tports));
-  // MED: the medium segments first in the list (4-lane groups), then the rest
+  // SM > 0: the medium segments first in the list, then the rest
+  constexpr bool MED = SM != 0;
   const bool lmed = MED && lng && pend <= (uint32_t)kStreamBase + kMedSpan;
   const uint64_t mm = MED ? __ballot(lmed) : 0ull, mb = MED ? m & ~mm : m;
   const uint32_t nmed = (uint32_t)__popcll(mm);
@@ -936,16 +955,17 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   }
   __builtin_amdgcn_wave_barrier();
   const uint32_t nlong = (uint32_t)__popcll(m);
-  const RoundPlan plan{nmed, nlong, MED ? (nmed + 64u / kMedG - 1u) / (64u / kMedG) : 0u};
-  const uint32_t R = plan.rm + (nlong - nmed + kRoundPk - 1) / kRoundPk;
+  const RoundPlan plan{nmed, nlong, SM == 1 ? (nmed + 64u / kMedG - 1u) / (64u / kMedG) : 0u};
+  const uint32_t R = SM == 2 ? (4u * ((nmed + 3u) & ~3u) + 16u * (nlong - nmed) + 63u) / 64u
+                             : plan.rm + (nlong - nmed + kRoundPk - 1) / kRoundPk;
   Round A, B;
-  round_issue<MED>(p, w, 0, plan, lane, A);
+  round_issue<SM>(p, w, 0, plan, lane, A);
 #pragma clang loop unroll(disable)
   for (uint32_t r = 0; r < R; r += 2) {
-    round_issue<MED>(p, w, r + 1, plan, lane, B);
-    round_finish<MED>(p, w, lane, A);
-    round_issue<MED>(p, w, r + 2, plan, lane, A);
-    round_finish<MED>(p, w, lane, B);
+    round_issue<SM>(p, w, r + 1, plan, lane, B);
+    round_finish<SM>(p, w, lane, A);
+    round_issue<SM>(p, w, r + 2, plan, lane, A);
+    round_finish<SM>(p, w, lane, B);
   }
   __builtin_amdgcn_wave_barrier();
   if (valid) {
@@ -1298,7 +1318,7 @@ ixg_rx_fastc_dmx_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, int MODE, bool MED = false>
+template <bool OFFS, bool EARLY, int MODE, int SM = 0>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
@@ -1315,7 +1335,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     gen_desc<OFFS>(p, c2, lane, D2);
     GPre P1;
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
-    deferred |= general_chunk<OFFS, MODE, BIG, MED>(p, T, c0, lane, w, D0, P0);
+    deferred |= general_chunk<OFFS, MODE, BIG, SM>(p, T, c0, lane, w, D0, P0);
     if (!EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
@@ -1331,7 +1351,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // fixed-shape kernel deferred as short or, in IXG_MODE_SHORT, walks every
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
-template <bool OFFS, uint32_t CLS, bool SEARLY = true, bool MED = false>
+template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -1397,9 +1417,9 @@ DEV void general_body(const KParams& p) {
     if (CLS == IXG_CLS_SHORT)
       seen |= gen_walk<OFFS, SEARLY, kModeFirst>(p, T, w, q, nq, lane, D0);
     else if (__any(D0.L > (uint32_t)kStreamBase + 32u))
-      gen_walk<OFFS, false, kModeLong, MED>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, false, kModeLong, SM>(p, T, w, q, nq, lane, D0);
     else
-      gen_walk<OFFS, true, kModeLong, MED>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, true, kModeLong, SM>(p, T, w, q, nq, lane, D0);
     __builtin_amdgcn_wave_barrier();
   }
   if (CLS == IXG_CLS_SHORT) publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
@@ -1414,8 +1434,8 @@ DEV void general_body(const KParams& p) {
 // the empty short dispatch on C2
 IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
 // (the default streams medium segments with 4-lane groups: C3 -5.5% in A/B)
-IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, true)
-IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, true)
+IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
@@ -1423,6 +1443,9 @@ IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, IXG_CLS_LONG, 4)
 // every long segment streamed by 16-lane groups (the split's A/B baseline)
 IXG_GEN_KERNEL(ixg_rx_general_g16_s, false, IXG_CLS_LONG, 2)
 IXG_GEN_KERNEL(ixg_rx_general_g16_o, true, IXG_CLS_LONG, 2)
+// packed stream mapping (SM 2)
+IXG_GEN_KERNEL(ixg_rx_general_pk_s, false, IXG_CLS_LONG, 2, true, 2)
+IXG_GEN_KERNEL(ixg_rx_general_pk_o, true, IXG_CLS_LONG, 2, true, 2)
 // the short-class general kernel (no streaming rounds); variants for A/B
 // (IXGRX_SHORT_VARIANT), index 0 the default
 IXG_GEN_KERNEL(ixg_rx_short_s, false, IXG_CLS_SHORT, 3)
@@ -1473,7 +1496,8 @@ static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
 static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
                                    {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
                                    {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
-                                   {ixg_rx_general_g16_s, ixg_rx_general_g16_o}};
+                                   {ixg_rx_general_g16_s, ixg_rx_general_g16_o},
+                                   {ixg_rx_general_pk_s, ixg_rx_general_pk_o}};
 static const kern_fn k_short[][2] = {{ixg_rx_short_s, ixg_rx_short_o},
                                      {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
                                      {ixg_rx_short_late_s, ixg_rx_short_late_o}};
