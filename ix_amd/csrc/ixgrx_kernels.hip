@@ -876,9 +876,14 @@ constexpr int kModeLong = 0, kModeFirst = 2;
 
 // BIG: big chunks take big_chunk (the walks without the one-ahead prefix
 // prefetch, so its registers are not live across the rounds)
-template <bool OFFS, int MODE, bool BIG, int SM = 0>
+// LATE (long mode without the one-ahead prefetch): the next chunk's prefix
+// (Dn -> Pn) is loaded here, after this chunk's last streaming round is
+// issued (its registers free by then), instead of after this chunk, where
+// the next chunk waited out its whole latency
+template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
-                       const WaveLds& w, const GDesc& g, const GPre& x) {
+                       const WaveLds& w, const GDesc& g, const GPre& x, const GDesc* Dn = nullptr,
+                       GPre* Pn = nullptr) {
   constexpr bool SHORT = MODE != kModeLong;
   const uint32_t i = chunk * 64u + (uint32_t)lane;
   const bool valid = i < p.n;
@@ -890,6 +895,7 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   }
   if (BIG && __all(g.L >= kBigMin || g.L == 0u)) {
     big_chunk<OFFS>(p, T, chunk, lane, w, g);
+    if (LATE) gen_pre<false, BIG>(p, *Dn, lane, *Pn);
     return false;
   }
   const uint64_t off = g.off;
@@ -917,6 +923,7 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   if (strm && !lng) s.l4_acc += piece_sum(v96, (int)rr);
   const uint64_t m = SHORT ? 0ull : __ballot(lng);
   if (SHORT || !m) {  // no long segment in this chunk (wave-uniform)
+    if (LATE) gen_pre<false, BIG>(p, *Dn, lane, *Pn);
     if (valid) {
       const uint32_t r4 = l4_residual(s);
       const Rec r = make_record(p, d, L, s, r4);
@@ -960,12 +967,29 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
                              : plan.rm + (nlong - nmed + kRoundPk - 1) / kRoundPk;
   Round A, B;
   round_issue<SM>(p, w, 0, plan, lane, A);
+  if (LATE) {
+    // pairs while more than two rounds remain, then the last one or two
+    // (a dummy B when one) with the next prefix issued behind them
+    uint32_t r = 0;
 #pragma clang loop unroll(disable)
-  for (uint32_t r = 0; r < R; r += 2) {
+    for (; r + 2 < R; r += 2) {
+      round_issue<SM>(p, w, r + 1, plan, lane, B);
+      round_finish<SM>(p, w, lane, A);
+      round_issue<SM>(p, w, r + 2, plan, lane, A);
+      round_finish<SM>(p, w, lane, B);
+    }
     round_issue<SM>(p, w, r + 1, plan, lane, B);
+    gen_pre<false, BIG>(p, *Dn, lane, *Pn);
     round_finish<SM>(p, w, lane, A);
-    round_issue<SM>(p, w, r + 2, plan, lane, A);
     round_finish<SM>(p, w, lane, B);
+  } else {
+#pragma clang loop unroll(disable)
+    for (uint32_t r = 0; r < R; r += 2) {
+      round_issue<SM>(p, w, r + 1, plan, lane, B);
+      round_finish<SM>(p, w, lane, A);
+      round_issue<SM>(p, w, r + 2, plan, lane, A);
+      round_finish<SM>(p, w, lane, B);
+    }
   }
   __builtin_amdgcn_wave_barrier();
   if (valid) {
@@ -1318,7 +1342,7 @@ ixg_rx_fastc_dmx_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, int MODE, int SM = 0>
+template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
@@ -1335,8 +1359,9 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     gen_desc<OFFS>(p, c2, lane, D2);
     GPre P1;
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
-    deferred |= general_chunk<OFFS, MODE, BIG, SM>(p, T, c0, lane, w, D0, P0);
-    if (!EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
+    constexpr bool LATE = LATE_OK && !EARLY && MODE == kModeLong;
+    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE>(p, T, c0, lane, w, D0, P0, &D1, &P1);
+    if (!EARLY && !LATE) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
     D0 = D1;
@@ -1351,7 +1376,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // fixed-shape kernel deferred as short or, in IXG_MODE_SHORT, walks every
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
-template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0>
+template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0, bool LATE = false>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -1417,7 +1442,7 @@ DEV void general_body(const KParams& p) {
     if (CLS == IXG_CLS_SHORT)
       seen |= gen_walk<OFFS, SEARLY, kModeFirst>(p, T, w, q, nq, lane, D0);
     else if (__any(D0.L > (uint32_t)kStreamBase + 32u))
-      gen_walk<OFFS, false, kModeLong, SM>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, false, kModeLong, SM, LATE>(p, T, w, q, nq, lane, D0);
     else
       gen_walk<OFFS, true, kModeLong, SM>(p, T, w, q, nq, lane, D0);
     __builtin_amdgcn_wave_barrier();
@@ -1433,9 +1458,10 @@ DEV void general_body(const KParams& p) {
 // chunks are nearly always short): one dispatch takes both classes, saving
 // the empty short dispatch on C2
 IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
-// (the default streams medium segments with 4-lane groups: C3 -5.5% in A/B)
-IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
-IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
+// (the default streams medium segments with 4-lane groups, C3 -5.5% in
+// A/B, and loads the next prefix behind the last round, C3 -1.2%)
+IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1, true)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1, true)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
@@ -1443,6 +1469,9 @@ IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, IXG_CLS_LONG, 4)
 // every long segment streamed by 16-lane groups (the split's A/B baseline)
 IXG_GEN_KERNEL(ixg_rx_general_g16_s, false, IXG_CLS_LONG, 2)
 IXG_GEN_KERNEL(ixg_rx_general_g16_o, true, IXG_CLS_LONG, 2)
+// the split without LATE (the next prefix loaded after the chunk)
+IXG_GEN_KERNEL(ixg_rx_general_nl_s, false, IXG_CLS_LONG, 2, true, 1)
+IXG_GEN_KERNEL(ixg_rx_general_nl_o, true, IXG_CLS_LONG, 2, true, 1)
 // packed stream mapping (SM 2)
 IXG_GEN_KERNEL(ixg_rx_general_pk_s, false, IXG_CLS_LONG, 2, true, 2)
 IXG_GEN_KERNEL(ixg_rx_general_pk_o, true, IXG_CLS_LONG, 2, true, 2)
@@ -1497,7 +1526,8 @@ static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
                                    {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
                                    {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
                                    {ixg_rx_general_g16_s, ixg_rx_general_g16_o},
-                                   {ixg_rx_general_pk_s, ixg_rx_general_pk_o}};
+                                   {ixg_rx_general_pk_s, ixg_rx_general_pk_o},
+                                   {ixg_rx_general_nl_s, ixg_rx_general_nl_o}};
 static const kern_fn k_short[][2] = {{ixg_rx_short_s, ixg_rx_short_o},
                                      {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
                                      {ixg_rx_short_late_s, ixg_rx_short_late_o}};
