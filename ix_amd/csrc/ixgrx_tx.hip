@@ -206,6 +206,13 @@ DEV void store16(uint64_t addr, const u32x4& v) { *reinterpret_cast<u32x4*>(addr
 // rate, so that path keeps default-policy stores)
 DEV void store16_nt(uint64_t addr, const u32x4& v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(addr)); }
 
+// rounds in flight in the streaming pass: 3 -> 1514-B frames 3.02 -> 2.89 ms
+// per 4M (same-process A/B), echo replies unchanged; 4 spills at 128 VGPRs
+#ifndef IXG_TX_RIF
+#define IXG_TX_RIF 3
+#endif
+constexpr int kTxRif = IXG_TX_RIF;
+
 // Pass B: G lanes per segment, 64 / G segments at a time.
 template <int G>
 DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
@@ -273,13 +280,13 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
         acc += piece_sum(sv, seg_len - 16 * (j + 1));
       }
     };
-    // two rounds' loads in flight per lane
-    for (int r = 0; __any(r < nr); r += 2) {
-      u32x4 v0, n0, v1, n1;
-      issue(r, v0, n0);
-      issue(r + 1, v1, n1);
-      round(r, v0, n0);
-      round(r + 1, v1, n1);
+    // kTxRif rounds' loads in flight per lane
+    for (int r = 0; __any(r < nr); r += kTxRif) {
+      u32x4 v[kTxRif], n[kTxRif];
+#pragma unroll
+      for (int q = 0; q < kTxRif; q++) issue(r + q, v[q], n[q]);
+#pragma unroll
+      for (int q = 0; q < kTxRif; q++) round(r + q, v[q], n[q]);
     }
     if (!udp) {
 #pragma unroll
