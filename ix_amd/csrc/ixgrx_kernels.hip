@@ -1458,10 +1458,10 @@ DEV void general_body(const KParams& p) {
 // chunks are nearly always short): one dispatch takes both classes, saving
 // the empty short dispatch on C2
 IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
-// (the default streams medium segments with 4-lane groups, C3 -5.5% in
-// A/B, and loads the next prefix behind the last round, C3 -1.2%)
-IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1, true)
-IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1, true)
+// (the default streams medium segments with 4-lane groups: C3 -5.5% in
+// A/B, and C3's FETCH_SIZE 6.64 -> 6.53 GB)
+IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
+IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
@@ -1469,9 +1469,10 @@ IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, IXG_CLS_LONG, 4)
 // every long segment streamed by 16-lane groups (the split's A/B baseline)
 IXG_GEN_KERNEL(ixg_rx_general_g16_s, false, IXG_CLS_LONG, 2)
 IXG_GEN_KERNEL(ixg_rx_general_g16_o, true, IXG_CLS_LONG, 2)
-// the split without LATE (the next prefix loaded after the chunk)
-IXG_GEN_KERNEL(ixg_rx_general_nl_s, false, IXG_CLS_LONG, 2, true, 1)
-IXG_GEN_KERNEL(ixg_rx_general_nl_o, true, IXG_CLS_LONG, 2, true, 1)
+// LATE: the next prefix loaded behind the last streaming round (C3 -1.2%
+// time but FETCH_SIZE +10%: 6.53 -> 7.18 GB per launch; not the default)
+IXG_GEN_KERNEL(ixg_rx_general_lt_s, false, IXG_CLS_LONG, 2, true, 1, true)
+IXG_GEN_KERNEL(ixg_rx_general_lt_o, true, IXG_CLS_LONG, 2, true, 1, true)
 // packed stream mapping (SM 2)
 IXG_GEN_KERNEL(ixg_rx_general_pk_s, false, IXG_CLS_LONG, 2, true, 2)
 IXG_GEN_KERNEL(ixg_rx_general_pk_o, true, IXG_CLS_LONG, 2, true, 2)
@@ -1527,7 +1528,7 @@ static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
                                    {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
                                    {ixg_rx_general_g16_s, ixg_rx_general_g16_o},
                                    {ixg_rx_general_pk_s, ixg_rx_general_pk_o},
-                                   {ixg_rx_general_nl_s, ixg_rx_general_nl_o}};
+                                   {ixg_rx_general_lt_s, ixg_rx_general_lt_o}};
 static const kern_fn k_short[][2] = {{ixg_rx_short_s, ixg_rx_short_o},
                                      {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
                                      {ixg_rx_short_late_s, ixg_rx_short_late_o}};
