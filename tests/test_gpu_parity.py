@@ -74,6 +74,7 @@ def test_golden_fixtures(golden, engines):
 @pytest.mark.parametrize("kind,n,flags", [
     ("tcp64", 50000, 0), ("imix", 30000, 0), ("tcp1514", 8000, 0), ("mixed", 30000, 0),
     ("mixed", 30000, ixgrx.IXG_F_IPV6), ("imix", 20000, ixgrx.IXG_F_NO_CSUM_DROP),
+    ("tcp64opt", 50000, 0),  # C2's 60-B slots, ihl 6: every coalesced chunk deferred
 ])
 def test_synthetic_vs_oracle(kind, n, flags, engines):
     tr = traces.make_trace(kind, n, seed=0x1B0000 + n, bad_ip=0.01, bad_l4=0.01)

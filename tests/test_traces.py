@@ -6,7 +6,7 @@ from ix_amd import traces
 from oracle import oracle
 
 
-@pytest.mark.parametrize("kind", ["tcp64", "imix", "tcp1514", "mixed"])
+@pytest.mark.parametrize("kind", ["tcp64", "tcp64opt", "imix", "tcp1514", "mixed"])
 def test_trace_valid(kind):
     tr = traces.make_trace(kind, 600, seed=0x1B0000 + 7)
     flags = 2 if kind == "mixed" else 0
@@ -19,6 +19,9 @@ def test_trace_valid(kind):
         assert (tr.len == 60).all() and (rec[:, 2] == 1).all()
     if kind == "tcp1514":
         assert (tr.len == 1514).all()
+    if kind == "tcp64opt":  # C2's slots, one IPv4 option word: never fixed-shape
+        assert (tr.len == 60).all() and tr.stride == 60 and (rec[:, 2] == 1).all()
+        assert (tr.blob[14::60][:tr.n] == 0x46).all()
 
 
 def test_trace_bad_fraction():
