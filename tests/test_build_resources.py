@@ -18,7 +18,7 @@ HIPCC = "/opt/rocm/bin/hipcc"
 SOURCES = ["ixgrx_kernels.hip", "ixgrx_tx.hip", "ixgrx_demux.hip", "ixgrx_ev.hip"]
 # A/B-only variants (IXGRX_GEN_VARIANT / IXGRX_SHORT_VARIANT, never launched
 # by default) built with occupancy targets that trade registers for waves
-AB_ONLY = re.compile(r"ixg_rx_(general_w[34]|short_w4|short_late)_[so]$")
+AB_ONLY = re.compile(r"ixg_rx_(general_w[34]|short_w4)_[so]$")
 
 
 def _resources(src):
