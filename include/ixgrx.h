@@ -179,6 +179,21 @@ int ixg_rx_hash_tables(const struct ixg_rx_cfg *cfg, uint64_t *tab12x256, uint32
 int ixg_abi_version(void);
 const char *ixg_strerror(int err);
 
+/* How the context's RX launches divide a batch between the kernels
+ * (DESIGN.md 4.1). AUTO, the default, is the only setting a drop-in needs:
+ * the others exist so tests can pin every kernel against the same oracle
+ * (each gives bit-identical records, only slower on some layouts). Nothing
+ * else (no environment variable) changes the launch plan. */
+enum ixg_split {
+	IXG_SPLIT_AUTO = 0,    /* device-side sampler / coalesced fixed-shape first */
+	IXG_SPLIT_FAST = 1,    /* fixed-shape kernel first, deferred chunks after */
+	IXG_SPLIT_SHORT = 2,   /* short kernel walks every chunk, defers long ones */
+	IXG_SPLIT_LONG = 3,    /* long kernel walks every chunk */
+	IXG_SPLIT_GENERAL = 4, /* long kernel alone, no defer flags */
+};
+/* 0 or -EINVAL. Applies to the context's later launches. */
+int ixg_rx_set_split(void *ctx, uint32_t split);
+
 /* ---- host-side dispatch: the eth_input replacement ------------------- */
 
 /* Callbacks a run-to-completion loop supplies; each receives the mbuf and

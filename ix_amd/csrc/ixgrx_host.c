@@ -34,6 +34,7 @@ struct ixg_slot {
 	struct ixg_dstate ds;
 	hipStream_t stream;
 	hipEvent_t done;
+	int ready;           /* every buffer below allocated (slot_init) */
 	int busy;            /* work enqueued, records not yet taken */
 	uint32_t first, n;   /* the chunk of the caller's batch it holds */
 	uint8_t *h_frames, *d_frames;
@@ -49,9 +50,11 @@ struct ixg_ctx {
 	struct ixg_rx_cfg cfg;
 	uint32_t crc_const;
 	uint32_t ncu;        /* compute units: persistent grids are sized from it */
-	int force_general;   /* IXGRX_FORCE_GENERAL=1: skip the fixed-shape kernel (tests/A-B) */
-	int fast_variant;    /* IXGRX_FAST_VARIANT=k: A/B of fixed-shape kernel builds */
-	uint32_t force_mode; /* IXGRX_MODE=fast|short|long: force the launch split (tests) */
+	int force_general;   /* IXG_SPLIT_GENERAL: skip the fixed-shape kernel (ixg_rx_set_split) */
+	int variant;         /* kernel variant selector: 0 in the product library; A/B
+	                        builds (-DIXGRX_AB, tools/build_variant.sh) read it
+	                        from IXGRX_*_VARIANT */
+	uint32_t force_mode; /* IXG_MODE_* forced by ixg_rx_set_split, or IXG_MODE_AUTO */
 	struct ixg_dstate ds; /* the synchronous and device-resident paths' */
 	struct ixg_slot slot[IXG_SLOTS];
 	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
@@ -264,26 +267,18 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 	hipDeviceProp_t prop;
 	if (hipGetDeviceProperties(&prop, device) != hipSuccess)
 		goto fail;
+	c->force_mode = IXG_MODE_AUTO;
+#ifdef IXGRX_AB
 	{
-		const char *e = getenv("IXGRX_FORCE_GENERAL");
-		c->force_general = e && e[0] == '1';
-		e = getenv("IXGRX_FAST_VARIANT");
-		c->fast_variant = e ? (atoi(e) & 0xff) : 0;
+		/* A/B builds only (never the product library) */
+		const char *e = getenv("IXGRX_FAST_VARIANT");
+		c->variant = e ? (atoi(e) & 0xff) : 0;
 		e = getenv("IXGRX_GEN_VARIANT");
-		c->fast_variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
+		c->variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
 		e = getenv("IXGRX_SHORT_VARIANT");
-		c->fast_variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
-		e = getenv("IXGRX_ANY_VARIANT");
-		c->fast_variant |= e ? ((atoi(e) & 0x7f) << 24) : 0;
-		e = getenv("IXGRX_MODE");
-		c->force_mode = IXG_MODE_AUTO;
-		if (e && !strcmp(e, "fast"))
-			c->force_mode = IXG_MODE_FAST;
-		else if (e && !strcmp(e, "short"))
-			c->force_mode = IXG_MODE_SHORT;
-		else if (e && !strcmp(e, "long"))
-			c->force_mode = IXG_MODE_LONG;
+		c->variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
 	}
+#endif
 	c->ncu = (uint32_t)prop.multiProcessorCount;
 	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
 	if (!tab) {
@@ -376,7 +371,18 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 		p.epoch = ds->epoch;
 		p.force_mode = c->force_mode;
 	}
-	return ixgrx_launch(&p, c->fast_variant, c->ncu, s) == 0 ? 0 : -EIO;
+	return ixgrx_launch(&p, c->variant, c->ncu, s) == 0 ? 0 : -EIO;
+}
+
+int ixg_rx_set_split(void *vctx, uint32_t split)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	static const uint32_t mode[] = {IXG_MODE_AUTO, IXG_MODE_FAST, IXG_MODE_SHORT, IXG_MODE_LONG, IXG_MODE_AUTO};
+	if (!c || split > IXG_SPLIT_GENERAL)
+		return -EINVAL;
+	c->force_general = split == IXG_SPLIT_GENERAL;
+	c->force_mode = mode[split];
+	return 0;
 }
 
 static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
@@ -404,9 +410,12 @@ int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, str
 
 static int grow_dev(struct ixg_ctx *c, size_t bytes, size_t n)
 {
+	/* a cap is set only once its buffers exist: a failed allocation leaves
+	 * cap 0, so the next call retries instead of launching on NULL */
 	if (bytes > c->d_frames_cap) {
 		hipFree(c->d_frames);
 		c->d_frames = NULL;
+		c->d_frames_cap = 0;
 		size_t cap = bytes + bytes / 4 + 4096;
 		HIPCHK(hipMalloc((void **)&c->d_frames, cap));
 		c->d_frames_cap = cap;
@@ -416,10 +425,14 @@ static int grow_dev(struct ixg_ctx *c, size_t bytes, size_t n)
 		hipFree(c->d_len);
 		hipFree(c->d_out);
 		hipFree(c->d_csum);
+		hipFree(c->d_dmx);
 		c->d_off = NULL;
 		c->d_len = NULL;
 		c->d_out = NULL;
 		c->d_csum = NULL;
+		c->d_dmx = NULL;
+		c->d_n_cap = 0;
+		c->d_dmx_cap = 0;
 		size_t cap = n + n / 4 + 64;
 		HIPCHK(hipMalloc((void **)&c->d_off, cap * sizeof(uint64_t)));
 		HIPCHK(hipMalloc((void **)&c->d_len, cap * sizeof(uint16_t)));
@@ -481,22 +494,38 @@ int ixg_rx_batch_host(void *vctx, const void *frames, const uint64_t *off, const
 
 static int slot_init(struct ixg_ctx *c, struct ixg_slot *sl)
 {
-	if (sl->stream)
+	/* ready only once every buffer exists: a failed allocation is retried
+	 * on the next call (buffers already made are kept, the rest made) */
+	if (sl->ready)
 		return 0;
-	HIPCHK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
-	HIPCHK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
-	HIPCHK(hipMalloc((void **)&sl->ds.d_present, 4 * sizeof(uint32_t)));
-	HIPCHK(hipMemset(sl->ds.d_present, 0, 4 * sizeof(uint32_t)));
-	sl->frames_cap = IXG_PIPE_BYTES + IXG_TAIL_PAD;
-	sl->n_cap = IXG_PIPE_FRAMES;
-	HIPCHK(hipHostMalloc((void **)&sl->h_frames, sl->frames_cap, hipHostMallocDefault));
-	HIPCHK(hipHostMalloc((void **)&sl->h_off, sl->n_cap * sizeof(uint64_t), hipHostMallocDefault));
-	HIPCHK(hipHostMalloc((void **)&sl->h_len, sl->n_cap * sizeof(uint16_t), hipHostMallocDefault));
-	HIPCHK(hipHostMalloc((void **)&sl->h_rec, sl->n_cap * sizeof(struct ixg_rx_rec), hipHostMallocDefault));
-	HIPCHK(hipMalloc((void **)&sl->d_frames, sl->frames_cap));
-	HIPCHK(hipMalloc((void **)&sl->d_off, sl->n_cap * sizeof(uint64_t)));
-	HIPCHK(hipMalloc((void **)&sl->d_len, sl->n_cap * sizeof(uint16_t)));
-	HIPCHK(hipMalloc((void **)&sl->d_rec, sl->n_cap * sizeof(struct ixg_rx_rec)));
+	if (!sl->stream)
+		HIPCHK(hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking));
+	if (!sl->done)
+		HIPCHK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
+	if (!sl->ds.d_present) {
+		HIPCHK(hipMalloc((void **)&sl->ds.d_present, 4 * sizeof(uint32_t)));
+		HIPCHK(hipMemset(sl->ds.d_present, 0, 4 * sizeof(uint32_t)));
+	}
+	const size_t fcap = IXG_PIPE_BYTES + IXG_TAIL_PAD, ncap = IXG_PIPE_FRAMES;
+	if (!sl->h_frames)
+		HIPCHK(hipHostMalloc((void **)&sl->h_frames, fcap, hipHostMallocDefault));
+	if (!sl->h_off)
+		HIPCHK(hipHostMalloc((void **)&sl->h_off, ncap * sizeof(uint64_t), hipHostMallocDefault));
+	if (!sl->h_len)
+		HIPCHK(hipHostMalloc((void **)&sl->h_len, ncap * sizeof(uint16_t), hipHostMallocDefault));
+	if (!sl->h_rec)
+		HIPCHK(hipHostMalloc((void **)&sl->h_rec, ncap * sizeof(struct ixg_rx_rec), hipHostMallocDefault));
+	if (!sl->d_frames)
+		HIPCHK(hipMalloc((void **)&sl->d_frames, fcap));
+	if (!sl->d_off)
+		HIPCHK(hipMalloc((void **)&sl->d_off, ncap * sizeof(uint64_t)));
+	if (!sl->d_len)
+		HIPCHK(hipMalloc((void **)&sl->d_len, ncap * sizeof(uint16_t)));
+	if (!sl->d_rec)
+		HIPCHK(hipMalloc((void **)&sl->d_rec, ncap * sizeof(struct ixg_rx_rec)));
+	sl->frames_cap = fcap;
+	sl->n_cap = ncap;
+	sl->ready = 1;
 	(void)c;
 	return 0;
 }
@@ -522,7 +551,7 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 	for (uint32_t i = 0; i < n; i++) {
 		size_t l;
 		memcpy(&l, mbufs[i], sizeof(l));
-		if (l > 0xffff)
+		if (l > IXG_MBUF_DATA_LEN) /* an mbuf holds at most 2048 data bytes (mbuf.h) */
 			return -EINVAL;
 	}
 	HIPCHK(hipSetDevice(c->device));
@@ -772,7 +801,7 @@ int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, co
 		c->d_dmx = NULL;
 		c->d_dmx_cap = 0;
 		HIPCHK(hipMalloc((void **)&c->d_dmx, (size_t)c->d_n_cap * sizeof(struct ixg_demux_rec)));
-		c->d_dmx_cap = c->d_n_cap;
+		c->d_dmx_cap = c->d_n_cap; /* grow_dev zeroes it whenever it reallocates */
 	}
 	HIPCHK(hipMemcpyAsync(c->d_frames, frames, (size_t)end, hipMemcpyHostToDevice, c->stream));
 	HIPCHK(hipMemsetAsync(c->d_frames + end, 0, IXG_TAIL_PAD, c->stream));
@@ -844,6 +873,7 @@ int ixg_tx_batch_dev(void *vctx, const void *seg_buf, const struct ixg_tx_seg *s
 		return -ENOENT;
 	if (n == 0)
 		return 0;
+	HIPCHK(hipSetDevice(c->device));
 	return tx_launch(c, seg_buf, segs, n, out, out_len, flags, (hipStream_t)stream);
 }
 
@@ -914,6 +944,7 @@ int ixg_ev_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ix
 		return -EINVAL;
 	if (n && (!fr->base || !d_rec || !d_ev || (d_dmx && n_pcbs && !d_pcbs) || (!fr->off && (fr->stride & 3))))
 		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
 	if (n == 0)
 		return hipMemsetAsync(d_count, 0, sizeof(uint32_t), (hipStream_t)stream) == hipSuccess ? 0 : -EIO;
 	/* scratch: chunk counts/bases, then group counts/bases (64 chunks a group) */

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 #include "../../include/ixgrx.h"
 #include "ixgrx_internal.h"
 #include "ixgrx_walk.h"
@@ -1154,16 +1156,19 @@ DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
     fast_loop<OFFS, AHEAD>(p, T);                                                   \
   }
 
-// variants for A/B (IXGRX_FAST_VARIANT); index 0 is the default.
 // _s: fixed-stride layout, _o: u64 offsets
 IXG_FAST_KERNEL(ixg_rx_fast_s, false, 1, 5)
 IXG_FAST_KERNEL(ixg_rx_fast_o, true, 1, 5)
+#ifdef IXGRX_AB
+// A/B builds only (tools/build_variant.sh; IXGRX_FAST_VARIANT): never in the
+// product library
 IXG_FAST_KERNEL(ixg_rx_fast_a2w4_s, false, 2, 4)
 IXG_FAST_KERNEL(ixg_rx_fast_a2w4_o, true, 2, 4)
 IXG_FAST_KERNEL(ixg_rx_fast_a2w5_s, false, 2, 5)
 IXG_FAST_KERNEL(ixg_rx_fast_a2w5_o, true, 2, 5)
 IXG_FAST_KERNEL(ixg_rx_fast_a1w4_s, false, 1, 4)
 IXG_FAST_KERNEL(ixg_rx_fast_a1w4_o, true, 1, 4)
+#endif
 
 // ---- fixed-shape kernel, coalesced (fixed stride <= 64 B) ---------------
 // A wave's 64 frames are one contiguous 64*stride-byte run. The wave loads
@@ -1453,7 +1458,6 @@ DEV void general_body(const KParams& p) {
 #define IXG_GEN_KERNEL(NAME, OFFS, CLS, WAVES, ...)                                                 \
   extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
   NAME(KParams p) { general_body<OFFS, CLS, ##__VA_ARGS__>(p); }
-// variants for A/B (IXGRX_GEN_VARIANT); index 0 is the default
 // behind the coalesced kernel (frames <= 64 B per stride, so deferred
 // chunks are nearly always short): one dispatch takes both classes, saving
 // the empty short dispatch on C2
@@ -1462,6 +1466,13 @@ IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
 // A/B, and C3's FETCH_SIZE 6.64 -> 6.53 GB)
 IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
 IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
+// the short-class general kernel (no streaming rounds): 4 waves/SIMD
+// without the one-ahead prefix prefetch (128 VGPRs; C5 -3% against the
+// 3-wave prefetching build)
+IXG_GEN_KERNEL(ixg_rx_short_late_s, false, IXG_CLS_SHORT, 4, false)
+IXG_GEN_KERNEL(ixg_rx_short_late_o, true, IXG_CLS_SHORT, 4, false)
+#ifdef IXGRX_AB
+// A/B builds only (IXGRX_GEN_VARIANT / IXGRX_SHORT_VARIANT)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
@@ -1476,14 +1487,11 @@ IXG_GEN_KERNEL(ixg_rx_general_lt_o, true, IXG_CLS_LONG, 2, true, 1, true)
 // packed stream mapping (SM 2)
 IXG_GEN_KERNEL(ixg_rx_general_pk_s, false, IXG_CLS_LONG, 2, true, 2)
 IXG_GEN_KERNEL(ixg_rx_general_pk_o, true, IXG_CLS_LONG, 2, true, 2)
-// the short-class general kernel (no streaming rounds); variants for A/B
-// (IXGRX_SHORT_VARIANT), index 0 the default
 IXG_GEN_KERNEL(ixg_rx_short_s, false, IXG_CLS_SHORT, 3)
 IXG_GEN_KERNEL(ixg_rx_short_o, true, IXG_CLS_SHORT, 3)
 IXG_GEN_KERNEL(ixg_rx_short_w4_s, false, IXG_CLS_SHORT, 4)
 IXG_GEN_KERNEL(ixg_rx_short_w4_o, true, IXG_CLS_SHORT, 4)
-IXG_GEN_KERNEL(ixg_rx_short_late_s, false, IXG_CLS_SHORT, 4, false)
-IXG_GEN_KERNEL(ixg_rx_short_late_o, true, IXG_CLS_SHORT, 4, false)
+#endif
 
 // The sampler: one block reads the lengths of up to 64 evenly spread chunks
 // and picks the launch's IXG_MODE_* (ixgrx_internal.h): FAST when at least
@@ -1518,43 +1526,48 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
 }
 
 typedef void (*kern_fn)(KParams);
-// [variant][layout: 0 = stride, 1 = offsets]
-static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o},
-                                    {ixg_rx_fast_a2w4_s, ixg_rx_fast_a2w4_o},
+// [variant][layout: 0 = stride, 1 = offsets]; the product library has only
+// variant 0 (the default kernels)
+static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o}
+#ifdef IXGRX_AB
+                                    , {ixg_rx_fast_a2w4_s, ixg_rx_fast_a2w4_o},
                                     {ixg_rx_fast_a2w5_s, ixg_rx_fast_a2w5_o},
-                                    {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}};
-static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o},
-                                   {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
+                                    {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}
+#endif
+};
+static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o}
+#ifdef IXGRX_AB
+                                   , {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
                                    {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
                                    {ixg_rx_general_g16_s, ixg_rx_general_g16_o},
                                    {ixg_rx_general_pk_s, ixg_rx_general_pk_o},
-                                   {ixg_rx_general_lt_s, ixg_rx_general_lt_o}};
-// default: 4 waves/SIMD without the one-ahead prefix prefetch (128 VGPRs;
-// C5 -3% against the 3-wave prefetching build, now variant 2)
-static const kern_fn k_short[][2] = {{ixg_rx_short_late_s, ixg_rx_short_late_o},
-                                     {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
-                                     {ixg_rx_short_s, ixg_rx_short_o}};
+                                   {ixg_rx_general_lt_s, ixg_rx_general_lt_o}
+#endif
+};
+static const kern_fn k_short[][2] = {{ixg_rx_short_late_s, ixg_rx_short_late_o}
+#ifdef IXGRX_AB
+                                     , {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
+                                     {ixg_rx_short_s, ixg_rx_short_o}
+#endif
+};
 static const int k_nshort = sizeof(k_short) / sizeof(k_short[0]);
 static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
 static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
 
+// blocks per CU, cached per (kernel, dynamic LDS): a handful of entries,
+// filled under a lock (contexts on several host threads launch concurrently)
 static int occupancy(kern_fn k, size_t shmem) {
-  // blocks per CU, cached per (kernel, dynamic LDS) (a handful; idempotent fill)
-  static kern_fn keys[32];
-  static size_t sizes[32];
-  static int vals[32];
-  for (int i = 0; i < 32; i++) {
-    if (keys[i] == k && sizes[i] == shmem) return vals[i];
-    if (!keys[i]) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, shmem) != hipSuccess || nb < 1) nb = 1;
-      vals[i] = nb;
-      sizes[i] = shmem;
-      keys[i] = k;
-      return nb;
-    }
-  }
-  return 1;
+  struct Entry { kern_fn k; size_t shmem; int nb; };
+  static std::mutex mu;
+  static Entry cache[32];
+  static int used = 0;
+  std::lock_guard<std::mutex> lock(mu);
+  for (int i = 0; i < used; i++)
+    if (cache[i].k == k && cache[i].shmem == shmem) return cache[i].nb;
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, shmem) != hipSuccess || nb < 1) nb = 1;
+  if (used < 32) cache[used++] = Entry{k, shmem, nb};
+  return nb;
 }
 
 static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 0) {
@@ -1569,7 +1582,7 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
 // 0's lane-load kernel.
 extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
-  int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff, av = (variant >> 24) & 0x7f;
+  int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff;
   if (gv >= k_ngen) gv = 0;
   if (sv >= k_nshort) sv = 0;
   const int lay = p.off ? 1 : 0;
@@ -1601,10 +1614,7 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   }
   const bool coal_any = p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0;
   if (coal_any) {
-    // any variant k > 0 (A/B): at most ncu / k blocks
-    const uint32_t acu = av ? (ncu / (uint32_t)av ? ncu / (uint32_t)av : 1u) : ncu;
-    hipLaunchKernelGGL(ixg_rx_any_s, dim3(av ? (group_blocks < acu ? (uint32_t)group_blocks : acu)
-                                             : grid_for(ixg_rx_any_s, group_blocks, ncu, sh6)), dim3(kBlock), sh6,
+    hipLaunchKernelGGL(ixg_rx_any_s, dim3(grid_for(ixg_rx_any_s, group_blocks, ncu, sh6)), dim3(kBlock), sh6,
                        (hipStream_t)stream, p);
     return (int)hipGetLastError();
   }

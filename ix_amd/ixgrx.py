@@ -48,8 +48,11 @@ EXPORTS = (
     "ixg_rx_hash_tables", "ixg_abi_version", "ixg_strerror", "ixg_rx_dispatch",
     "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg_rx_demux_batch_dev",
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
-    "ixg_ev_batch_dev",
+    "ixg_ev_batch_dev", "ixg_rx_set_split",
 )
+
+# enum ixg_split (ixg_rx_set_split): how a context's launches divide a batch
+SPLITS = {"auto": 0, "fast": 1, "short": 2, "long": 3, "general": 4}
 
 
 class RxCfg(ctypes.Structure):
@@ -121,6 +124,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_strerror.restype = ctypes.c_char_p
     lib.ixg_rx_dispatch.argtypes = [vp, vp, u32, vp, vp]
     lib.ixg_rx_dispatch.restype = u32
+    lib.ixg_rx_set_split.argtypes = [vp, u32]
+    lib.ixg_rx_set_split.restype = i32
     if lib.ixg_abi_version() != ABI_VERSION:
         raise RuntimeError("libixgrx ABI version mismatch")
     _libs[path] = lib
@@ -146,16 +151,23 @@ def hash_tables(cfg: Config) -> tuple[np.ndarray, int]:
 @dataclass
 class RxEngine:
     """One ixg_rx context on HIP device `device` (lib_path: another build of
-    the library, for A/B timing; default ix_amd/libixgrx.so)."""
+    the library, for A/B timing; default ix_amd/libixgrx.so). `split`: the
+    launch split (SPLITS; ixg_rx_set_split), "auto" for the drop-in."""
     cfg: Config
     device: int = 0
     lib_path: str = LIB_PATH
+    split: str = "auto"
     _ctx: ctypes.c_void_p = field(default_factory=ctypes.c_void_p, init=False)
 
     def __post_init__(self):
         self._lib = lib = load_library(self.lib_path)
         self._ccfg = self.cfg.to_c()
         _check(lib.ixg_rx_init(ctypes.byref(self._ccfg), self.device, ctypes.byref(self._ctx)), "ixg_rx_init", lib)
+        if self.split != "auto":
+            self.set_split(self.split)
+
+    def set_split(self, split: str) -> None:
+        _check(self._lib.ixg_rx_set_split(self._ctx, SPLITS[split]), "ixg_rx_set_split", self._lib)
 
     def close(self) -> None:
         if self._ctx:

@@ -14,6 +14,23 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    _use_sanitized_builds()
+
+
+def _use_sanitized_builds():
+    """tests/test_sanitize.py re-runs the CPU tier with the ASan/UBSan builds
+    of the host library and the oracle: it names them in IXG_SAN_LIB /
+    IXG_SAN_ORACLE, and they are installed here under the default paths'
+    cache keys (test harness only; the product binding has no such switch)."""
+    lib, orc = os.environ.get("IXG_SAN_LIB"), os.environ.get("IXG_SAN_ORACLE")
+    if not (lib and orc):
+        return
+    from ix_amd import ixgrx
+    from oracle import oracle
+    ixgrx._libs[os.path.abspath(ixgrx.LIB_PATH)] = ixgrx.load_library(lib)
+    oracle.LIB = orc
+    oracle._lib = None
+    print("sanitized builds in use:", lib, orc)
 
 
 def golden_names(prefix: str = ""):

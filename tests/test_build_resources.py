@@ -16,9 +16,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "ix_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 SOURCES = ["ixgrx_kernels.hip", "ixgrx_tx.hip", "ixgrx_demux.hip", "ixgrx_ev.hip"]
-# A/B-only variants (IXGRX_GEN_VARIANT / IXGRX_SHORT_VARIANT, never launched
-# by default) built with occupancy targets that trade registers for waves
-AB_ONLY = re.compile(r"ixg_rx_(general_w[34]|short_w4)_[so]$")
+# A/B-only variants (built only with -DIXGRX_AB: tools/build_variant.sh)
+AB_ONLY = re.compile(r"ixg_rx_(general_(w[34]|g16|lt|pk)|short_(w4|[so]$)|fast_a\d)")
 
 
 def _resources(src):
@@ -46,3 +45,20 @@ def test_no_scratch(src):
     bad = {k: v for k, v in res.items()
            if not AB_ONLY.search(k) and (v.get("ScratchSize [bytes/lane]", 0) or v.get("VGPRs Spill", 0))}
     assert not bad, f"kernels with scratch / spills in {src}: {bad}"
+
+
+def test_product_library_has_no_ab_code():
+    """The product library carries only the kernels ixgrx_launch dispatches
+    and reads no environment: A/B variants and their IXGRX_* knobs exist only
+    in -DIXGRX_AB builds (tools/build_variant.sh), so nothing but
+    ixg_rx_set_split changes a context's launch plan."""
+    lib = os.path.join(os.path.dirname(HERE), "ix_amd", "libixgrx.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    syms = subprocess.run(["nm", "-D", lib], capture_output=True, text=True, check=True).stdout
+    kernels = sorted(set(re.findall(r"__device_stub__(\w+)", syms)))
+    assert kernels and not [k for k in kernels if AB_ONLY.search(k)], kernels
+    undefined = subprocess.run(["nm", "-D", "--undefined-only", lib], capture_output=True, text=True,
+                               check=True).stdout.split()
+    assert "getenv" not in undefined and "secure_getenv" not in undefined
+

@@ -190,20 +190,8 @@ def test_gpu_demux_requires_tables():
 
 
 def _engine_in_mode(cfg, mode):
-    """An engine with the launch split forced (IXGRX_MODE / IXGRX_FORCE_GENERAL)."""
-    import os
-    env = {"IXGRX_FORCE_GENERAL": "1" if mode == "general" else "0",
-           "IXGRX_MODE": mode if mode in ("fast", "short", "long") else "auto"}
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return ixgrx.RxEngine(cfg)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    """An engine with the launch split forced (ixg_rx_set_split)."""
+    return ixgrx.RxEngine(cfg, split=mode)
 
 
 def _fused_dev(eng, blob, off, lens, stride, n):

@@ -37,26 +37,15 @@ def _diff(got, exp, what):
 @pytest.fixture(scope="module", params=["auto", "general", "fast", "short", "long"])
 def engines(request):
     """Engines on the default path (the device-side sampler picks the split),
-    with IXGRX_FORCE_GENERAL=1 (general kernel only, no defer flags), and
-    with each launch split forced (IXGRX_MODE): fixed-shape kernel first,
-    short kernel walking every chunk, long kernel walking every chunk."""
+    with the general kernel alone (no defer flags), and with each launch
+    split forced (ixg_rx_set_split): fixed-shape kernel first, short kernel
+    walking every chunk, long kernel walking every chunk."""
     cache = {}
-    env = {"IXGRX_FORCE_GENERAL": "1" if request.param == "general" else "0",
-           "IXGRX_MODE": request.param if request.param in ("fast", "short", "long") else "auto"}
 
     def get(key=KEY, nb=128, dev=0, flags=0):
         k = (bytes(key), nb, dev, flags)
         if k not in cache:
-            old = {v: os.environ.get(v) for v in env}
-            os.environ.update(env)
-            try:
-                cache[k] = ixgrx.RxEngine(ixgrx.Config(bytes(key), nb, dev, flags))
-            finally:
-                for v, o in old.items():
-                    if o is None:
-                        del os.environ[v]
-                    else:
-                        os.environ[v] = o
+            cache[k] = ixgrx.RxEngine(ixgrx.Config(bytes(key), nb, dev, flags), split=request.param)
         return cache[k]
     yield get
     for e in cache.values():
@@ -404,3 +393,77 @@ def test_hip_graph_replay(kind):
             _diff(out.cpu().numpy(), er, f"graph replay {kind}")
     finally:
         eng.close()
+
+
+def test_hip_graph_replay_mode_change():
+    """One captured launch over a fixed slot layout (u64 offsets, 1536-B
+    slots) replayed over batches that the device-side sampler sends down
+    different splits: 64-B frames (FAST), 1514-B frames (LONG), short
+    option-laden / IPv6-free mixed frames (SHORT) and back. A replay reuses
+    the captured class stamps, so a later replay can see classes a previous
+    one deferred; every record must still be the oracle's."""
+    import torch
+    n, S = 12288, 1536
+    kinds = ["tcp64", "tcp1514", "mixed", "tcp64", "imix", "tcp1514"]
+    batches = []
+    for k, kind in enumerate(kinds):
+        t = traces.make_trace(kind, n, seed=0x1B7000 + k)
+        offs = t.offsets().astype(np.int64)
+        blob = np.zeros(n * S + 64, np.uint8)
+        for i in range(n):
+            L = int(t.len[i])
+            blob[i * S:i * S + L] = t.blob[offs[i]:offs[i] + L]
+        batches.append(traces.Trace(blob, np.arange(n, dtype=np.uint64) * S, t.len.copy(), 0))
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY, 128, 0, 0))
+    try:
+        dev = torch.device("cuda:0")
+        blob = torch.zeros(n * S + 64, dtype=torch.uint8, device=dev)
+        off = torch.from_numpy(batches[0].off.view(np.int64)).to(dev)
+        lens = torch.zeros(n, dtype=torch.int16, device=dev)
+        out = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+
+        def load(t):
+            blob.copy_(torch.from_numpy(t.blob))
+            lens.copy_(torch.from_numpy(t.len.view(np.int16)))
+        load(batches[0])
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            eng.batch_dev(blob.data_ptr(), off.data_ptr(), lens.data_ptr(), 0, n, out.data_ptr(), None,
+                          s.cuda_stream)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            eng.batch_dev(blob.data_ptr(), off.data_ptr(), lens.data_ptr(), 0, n, out.data_ptr(), None,
+                          s.cuda_stream)
+        for kind, t in zip(kinds, batches):
+            load(t)
+            out.zero_()
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            er, _ = oracle.rx_trace(t, KEY, threads=8)
+            _diff(out.cpu().numpy(), er, f"graph replay, {kind} batch")
+    finally:
+        eng.close()
+
+
+def test_mbufs_reject_oversized_len():
+    """An IX mbuf holds at most 2048 data bytes (IXG_MBUF_DATA_LEN): a larger
+    mbuf->len is -EINVAL, not a gather of the next mbuf's bytes."""
+    tr = traces.make_trace("tcp64", 256, seed=0x1B7100)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY))
+    try:
+        rec = eng.batch_mbufs(ptrs)
+        er, _ = oracle.rx_trace(tr, KEY)
+        _diff(rec, er, "mbufs")
+        base = int(ptrs[37]) - arena.ctypes.data
+        for bad in (2049, 4096, 0xffff, 1 << 40):
+            arena[base:base + 8] = np.frombuffer(np.uint64(bad).tobytes(), np.uint8)
+            with pytest.raises(RuntimeError, match="invalid argument"):
+                eng.batch_mbufs(ptrs)
+        arena[base:base + 8] = np.frombuffer(np.uint64(2048).tobytes(), np.uint8)
+        eng.batch_mbufs(ptrs)  # the maximum itself is accepted
+    finally:
+        eng.close()
+

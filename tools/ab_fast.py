@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--lib", default="tools/ablib/ab.so", help="an A/B build (make -C ix_amd/csrc AB=1 OUT=...)")
     args = ap.parse_args()
     import torch
     import bench
@@ -33,13 +34,13 @@ def main():
     for v in args.variants.split(","):
         # "3" = fast variant 3; "0:1" = fast variant 0 + general variant 1;
         # "0:0:2" = + short variant 2; "g1" = general-only with general variant 1
-        os.environ["IXGRX_FORCE_GENERAL"] = "1" if v.startswith("g") else "0"
+        # (variants exist only in an A/B build: make -C ix_amd/csrc AB=1 OUT=...)
         parts = (["0", v[1:] or "0"] if v.startswith("g") else v.split(":")) + ["0", "0"]
         os.environ["IXGRX_FAST_VARIANT"] = parts[0] or "0"
         os.environ["IXGRX_GEN_VARIANT"] = parts[1] or "0"
         os.environ["IXGRX_SHORT_VARIANT"] = parts[2] or "0"
-        os.environ["IXGRX_ANY_VARIANT"] = (parts[3] if len(parts) > 3 else "0") or "0"
-        engs[v] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags))
+        engs[v] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags), lib_path=os.path.join(ROOT, args.lib),
+                                 split="general" if v.startswith("g") else "auto")
     s = torch.cuda.current_stream()
     times = {v: [] for v in engs}
     # parity: every variant's records equal the first variant's, and each

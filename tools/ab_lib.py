@@ -23,18 +23,18 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--k", type=int, default=10)
-    ap.add_argument("--general", action="store_true", help="IXGRX_FORCE_GENERAL=1 for every build")
+    ap.add_argument("--general", action="store_true", help="general kernel alone (ixg_rx_set_split) for every build")
     args = ap.parse_args()
     import torch
     import bench
     from ix_amd import ixgrx, traces
     dev = torch.device("cuda:0")
     wl = bench.Workload(args.workload, seed=0x1B0002, dev=dev)
-    os.environ["IXGRX_FORCE_GENERAL"] = "1" if args.general else "0"
     engs = {}
     for path in args.libs.split(","):
         engs[os.path.basename(path)] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags),
-                                                      lib_path=os.path.join(ROOT, path))
+                                                      lib_path=os.path.join(ROOT, path),
+                                                      split="general" if args.general else "auto")
     s = torch.cuda.current_stream()
     # parity: every build's records equal the first build's, and each tiled
     # batch is self-consistent (the oracle checks the first build in tests/)

@@ -11,9 +11,8 @@ for pl in range(40, 80):
     frames.append(mg.ipv4(proto=6, payload=bytes((7 * k + 3) & 0xff for k in range(pl))))
 tr = traces.pack(frames)
 er, ec = oracle.rx_trace(tr, traces.RSS_KEY)
-for mode in ("0", "1"):
-    os.environ["IXGRX_FORCE_GENERAL"] = mode
-    e = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY))
+for mode in ("auto", "general"):
+    e = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY), split=mode)
     rec, cs = e.batch_trace(tr, want_csum=True)
     for k in range(len(frames)):
         L = len(frames[k])
