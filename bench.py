@@ -49,7 +49,12 @@ WORKLOADS = {
     "c2": ("tcp64", 16 * 1024 * 1024, 1 << 20, "C2: 16M x 64B Eth/IPv4/TCP frames (L=60, stride 60), 1 GPU"),
     "c4": ("tcp1514", 8 * 1024 * 1024, 1 << 13, "C4 per-GPU shard: 8M x 1514B IPv4/TCP frames (stride 1516)"),
     "c3": ("imix", 16 * 1024 * 1024, 1 << 18, "C3: 16M IMIX 7:4:1 (60/590/1514B) TCP+UDP, packed, u64 offsets"),
-    "c5": ("mixed", 16 * 1024 * 1024, 1 << 18, "C5: 16M mixed IPv4 ihl 5..15 + 50% IPv6, packed"),
+    "c5": ("mixed", 16 * 1024 * 1024, 1 << 18, "C5: 16M mixed IPv4 ihl 5..15 + 50% IPv6 (IXG_F_IPV6 extension: IPv6 "
+                                                "parsed), packed"),
+    # C5 in the reference's semantics: IPv6 frames are dropped by eth_input
+    # (dp/net/ip.c:132-137), IPv4 with options parsed
+    "c5r": ("mixed", 16 * 1024 * 1024, 1 << 18, "C5 (reference semantics: IPv6 -> DROP_ETHERTYPE): 16M mixed IPv4 "
+                                                 "ihl 5..15 + 50% IPv6, packed"),
     # A/B only (not configs): C5's families alone or in 128-frame runs
     "c5v4": ("mixed_v4", 16 * 1024 * 1024, 1 << 18, "C5 IPv4 part only (A/B only)"),
     "c5v6": ("mixed_v6", 16 * 1024 * 1024, 1 << 18, "C5 IPv6 part only (A/B only)"),
@@ -63,16 +68,17 @@ WORKLOADS = {
 }
 
 
-def alg_bytes(tr) -> np.ndarray:
+def alg_bytes(tr, flags: int = 0) -> np.ndarray:
     """Algorithmic bytes read per frame: 14 + ip_len for
     IPv4 (the Ethernet header plus the IP datagram; padding excluded), 54 +
-    payload for IPv6, plus the descriptor and the 16-byte record."""
+    payload for IPv6 under IXG_F_IPV6 (else 14: eth_input drops it on the
+    ethertype), plus the descriptor and the 16-byte record."""
     offs = tr.offsets().astype(np.int64)
     b = tr.blob
     et = (b[offs + 12].astype(np.int64) << 8) | b[offs + 13]
     v4 = (b[offs + 16].astype(np.int64) << 8) | b[offs + 17]
     v6 = (b[offs + 18].astype(np.int64) << 8) | b[offs + 19]
-    rd = np.where(et == 0x86DD, 54 + v6, 14 + v4)
+    rd = np.where(et == 0x86DD, 54 + v6 if flags & 2 else 14, 14 + v4)
     rd = np.minimum(rd, tr.len.astype(np.int64))
     desc = 2 + (8 if tr.off is not None else 0)
     return rd + desc + 16
@@ -95,9 +101,9 @@ class Workload:
         if name == "c2o":
             tr = self.pool
             self.pool = traces.Trace(tr.blob, tr.offsets().copy(), tr.len, 0)
-        self.flags = 2 if kind.startswith("mixed") else 0
+        self.flags = 2 if kind.startswith("mixed") and name != "c5r" else 0
         tr = self.pool
-        self.bytes_per_pkt = float(alg_bytes(tr).mean())
+        self.bytes_per_pkt = float(alg_bytes(tr, self.flags).mean())
         self.wire_bytes = float(tr.len.astype(np.int64).mean())
         if tr.off is None:
             S = tr.stride
@@ -191,30 +197,56 @@ def cpu_rate(ptrs, flags, key, seconds, threads, hash_mode, work):
 
 
 def cpu_baseline(tr, flags, key, seconds: float, threads: int, name: str):
-    """The oracle (C restatement) on host cores over a bounded sample of the
-    workload: its distinct frames (up to 2^20) in IX mbufs, repeated for
-    `seconds`. `value` = full software work (parse + IP/L4 checksums +
-    Toeplitz + tcp_to_idx, table-driven hashes) on `threads` threads; the
-    1-core modes of BASELINE.md's CPU plan and the reference's own code
-    (oracle/_ref, 1 core) are reported beside it."""
+    """dp/ix's own RX path on the GPU box's host cores:
+    oracle/_ref/ixref_bench, built from the reference's dp/net + dp/lwip
+    sources (oracle/ref_harness/harness_bench.c), one process per core, each
+    over its own arena of pre-filled 2112-B IX mbufs larger than the LLC.
+    `value` = IX's per-packet software work as deployed (eth_input -> ip_input
+    -> tcp_input_tmp -> tcp_input head with tcp_to_idx; checksums and RSS are
+    the NIC's); "full_software" adds the reference's checksum and Toeplitz
+    functions (the work the GPU kernels do). The oracle (C restatement, the
+    "port") is timed beside it. Falls back to the port when the reference
+    binary was not built."""
     from oracle import oracle
+    procs = threads
+    mb = 1 << 18  # 553 MB of mbufs per core: beyond the LLC, as fresh DMA'd packets
+    ix = oracle.ref_bench(tr, key, "ix", procs, seconds, mb) if flags == 0 else None
+    res = {}
+    if ix is not None:
+        full = oracle.ref_bench(tr, key, "full", procs, max(2.0, seconds / 2), mb)
+        one = oracle.ref_bench(tr, key, "ix", 1, max(2.0, seconds / 4), mb)
+        res = {"value": round(ix["mpps"], 2), "unit": "Mpkt/s", "cores": procs, "kind": "reference",
+               "sample": f"oracle/_ref/ixref_bench ix: the reference's eth_input -> ip_input -> tcp_input_tmp -> "
+                         f"tcp_input head + tcp_to_idx (NIC checksum/RSS offload as in IX) over {ix['frames']} "
+                         f"distinct {name} frames in {mb} pre-filled 2112-B IX mbufs per core, {ix['pkts']:.0f} "
+                         f"frames in {ix['seconds']:.1f}s on {procs} processes",
+               "ns_per_pkt_core": ix["ns_per_pkt_core"],
+               "full_software": {"mpps": round(full["mpps"], 2), "cores": procs,
+                                 "ns_per_pkt_core": full["ns_per_pkt_core"],
+                                 "what": "+ the reference's chksum_internet, inet_chksum_pseudo_partial and "
+                                         "compute_toeplitz_hash per frame (the NIC's work in software)"},
+               "reference_1core": {"mpps": round(one["mpps"], 2), "ns_per_pkt": one["ns_per_pkt_core"]}}
     n = min(tr.n, 1 << 20)
     arena, ptrs = mbuf_arena(tr, n)
-    v, done, secs = cpu_rate(ptrs, flags, key, seconds, threads, oracle.HASH_TABLE, oracle.WORK_FULL)
-    side = max(1.0, seconds / 6)
+    v, done, secs = cpu_rate(ptrs, flags, key, max(2.0, seconds / 2), threads, oracle.HASH_TABLE, oracle.WORK_FULL)
+    side = max(1.0, seconds / 8)
     one = {}
     for label, hm, wk in (("full_table", oracle.HASH_TABLE, oracle.WORK_FULL),
                           ("full_bitserial", oracle.HASH_BITSERIAL, oracle.WORK_FULL),
                           ("ix_equivalent", oracle.HASH_TABLE, oracle.WORK_IX)):
         one[label] = round(cpu_rate(ptrs[:1 << 16], flags, key, side, 1, hm, wk)[0], 2)
     del arena
-    ref, rdesc = oracle.ref_time(tr, key, side, flags=flags)
-    return {"value": round(v, 2), "unit": "Mpkt/s", "cores": threads, "kind": "port",
+    port = {"mpps": round(v, 2), "cores": threads,
             "sample": f"oracle/ixgrx_oracle.c full software (table-driven Toeplitz/CRC) over {n} {name} frames "
                       f"in 2112-B IX mbufs, {done} frames in {secs:.1f}s on {threads} threads",
-            "modes_1core_mpps": one,
-            "reference_1core_mpps": None if ref is None else round(ref / 1e6, 2),
-            "reference_sample": rdesc}
+            "modes_1core_mpps": one}
+    if not res:
+        res = {"value": port["mpps"], "unit": "Mpkt/s", "cores": threads, "kind": "port", "sample": port["sample"],
+               "modes_1core_mpps": one,
+               "note": "oracle/_ref/ixref_bench not built (or not an IPv4-only workload): the port is the baseline"}
+    else:
+        res["port"] = port
+    return res
 
 
 def parity_leg(checks, key) -> dict:

@@ -60,6 +60,8 @@ struct ixg_ctx {
 	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
 	uint64_t *d_tab;
 	uint32_t *d_tab6;
+	uint32_t *d_tab32;   /* d_tab split: Toeplitz words, CRC low halves */
+	uint16_t *d_tab16;
 	hipStream_t stream; /* for the synchronous host paths */
 	/* host-path device staging (ixg_rx_batch_host, ixg_demux_batch_host) */
 	uint8_t *d_frames;
@@ -151,16 +153,14 @@ int ixg_rx_hash_tables(const struct ixg_rx_cfg *cfg, uint64_t *tab, uint32_t *cr
 	return 0;
 }
 
-/* IXG_TAB6_WORDS: for tuple byte i, [2i][n] = the contribution of high
- * nibble n, [2i+1][n] = that of low nibble n (Toeplitz is linear, so a byte's
- * contribution is the XOR of its two nibbles') */
+/* IXG_TAB6_WORDS: [i - IXG_TAB6_FIRST][v] = the Toeplitz contribution of
+ * value v at tuple byte i of the 36-byte IPv6 tuple, for i = 12..35 (bytes
+ * 0..11 share the IPv4 tables' key offsets) */
 static void hash_table6(const struct ixg_rx_cfg *cfg, uint32_t *tab6)
 {
-	for (int i = 0; i < 36; i++)
-		for (unsigned v = 0; v < 16; v++) {
-			tab6[(2 * i) * 16 + v] = toeplitz_byte(cfg->rss_key, i, v << 4);
-			tab6[(2 * i + 1) * 16 + v] = toeplitz_byte(cfg->rss_key, i, v);
-		}
+	for (unsigned i = IXG_TAB6_FIRST; i < 36; i++)
+		for (unsigned v = 0; v < 256; v++)
+			tab6[(i - IXG_TAB6_FIRST) * 256 + v] = toeplitz_byte(cfg->rss_key, (int)i, v);
 }
 
 /* ---- context -------------------------------------------------------------- */
@@ -196,6 +196,8 @@ void ixg_rx_fini(void *vctx)
 		hipStreamSynchronize(c->stream);
 	hipFree(c->d_tab);
 	hipFree(c->d_tab6);
+	hipFree(c->d_tab32);
+	hipFree(c->d_tab16);
 	hipFree(c->ds.d_defer);
 	hipFree(c->d_zero);
 	hipFree(c->ds.d_present);
@@ -286,8 +288,18 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		goto fail;
 	}
 	ixg_rx_hash_tables(cfg, tab, &c->crc_const);
+	uint32_t tab32[12 * 256];
+	uint16_t tab16[12 * 256];
+	for (int k = 0; k < 12 * 256; k++) {
+		tab32[k] = (uint32_t)tab[k];
+		tab16[k] = (uint16_t)(tab[k] >> 32);
+	}
 	if (hipMalloc((void **)&c->d_tab, 12 * 256 * sizeof(uint64_t)) != hipSuccess ||
-	    hipMemcpy(c->d_tab, tab, 12 * 256 * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess) {
+	    hipMemcpy(c->d_tab, tab, 12 * 256 * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMalloc((void **)&c->d_tab32, sizeof(tab32)) != hipSuccess ||
+	    hipMemcpy(c->d_tab32, tab32, sizeof(tab32), hipMemcpyHostToDevice) != hipSuccess ||
+	    hipMalloc((void **)&c->d_tab16, sizeof(tab16)) != hipSuccess ||
+	    hipMemcpy(c->d_tab16, tab16, sizeof(tab16), hipMemcpyHostToDevice) != hipSuccess) {
 		free(tab);
 		goto fail;
 	}
@@ -335,6 +347,8 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 	p.csum = csum;
 	p.tab = c->d_tab;
 	p.tab6 = c->d_tab6;
+	p.tab32 = c->d_tab32;
+	p.tab16 = c->d_tab16;
 	p.stride = stride;
 	p.n = n;
 	p.crc_const = c->crc_const;

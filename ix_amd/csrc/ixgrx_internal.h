@@ -19,7 +19,9 @@ struct ixg_kparams {
 	struct ixg_rx_rec *out;
 	uint32_t *csum;
 	const uint64_t *tab;   /* 12 x 256: lo = Toeplitz, hi = CRC-32C contribution */
-	const uint32_t *tab6;  /* IXG_TAB6_WORDS nibble Toeplitz contributions (IXG_F_IPV6), or NULL */
+	const uint32_t *tab6;  /* IXG_TAB6_WORDS Toeplitz contributions of tuple bytes 12..35 (IXG_F_IPV6), or NULL */
+	const uint32_t *tab32; /* tab's low words (Toeplitz), 12 x 256 */
+	const uint16_t *tab16; /* tab's high words' low halves (CRC-32C; the bucket needs 9 bits), 12 x 256 */
 	uint32_t stride;
 	uint32_t n;
 	uint32_t crc_const;
@@ -73,11 +75,11 @@ typedef struct ixg_kparams ixg_kparams;
 #define IXG_MODE_LONG 2u
 #define IXG_MODE_AUTO 0xffffffffu
 
-/* The IPv6-extension Toeplitz table (ixg_kparams.tab6): per input byte of
- * the 36-byte tuple, 16 entries for its high nibble and 16 for its low one
- * (72 x 16 u32 = 4.5 KiB), so the general kernels' LDS copy leaves room for
- * 3 workgroups per CU instead of 2 with a 36 KiB byte table */
-#define IXG_TAB6_WORDS (72u * 16u)
+/* The IPv6-extension Toeplitz tables (ixg_kparams.tab6): the contribution
+ * of each value of tuple bytes 12..35 (24 x 256 u32 = 24 KiB); tuple bytes
+ * 0..11 use the IPv4 tables' Toeplitz words (the same key offsets) */
+#define IXG_TAB6_FIRST 12u
+#define IXG_TAB6_WORDS (24u * 256u)
 
 /* implemented in ixgrx_kernels.hip */
 /* enqueue one batch: the fixed-shape kernel (when p->defer) and the general

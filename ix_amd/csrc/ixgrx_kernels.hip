@@ -35,6 +35,12 @@
 
 #define DEV __device__ __forceinline__
 
+// Wave votes from one v_cmp into an SGPR pair + a scalar compare (the ockl
+// __all/__any helpers cost several VALU instructions each). Inactive lanes
+// do not vote, as with __all/__any.
+DEV bool wave_all(bool pred) { return __builtin_amdgcn_ballot_w64(!pred) == 0; }
+DEV bool wave_any(bool pred) { return __builtin_amdgcn_ballot_w64(pred) != 0; }
+
 namespace {
 
 constexpr int kBlock = 256;        // 4 waves
@@ -225,14 +231,45 @@ struct LaneState {
   uint32_t src, dst, ports;
 };
 
-// FIXED: every lane is IPv4 with ihl 5 (wave-uniform), so the header
-// geometry is constant-folded. NDW: prefix dwords available; a segment
-// ending past 4*NDW bytes is left to the streaming rounds.
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// x & ones(clamp(t, 0, 4)): v_med3 + two shifts (the 64-bit one handles
+// the shift by 32) + v_bfi
+DEV uint32_t keep_bytes(uint32_t x, int t) {
+  const uint32_t u = (uint32_t)(t < 0 ? 0 : (t > 4 ? 4 : t));
+  return x & ~(uint32_t)(~0ull << (8u * u));
+}
 
-template <bool FIXED, int NDW>
-DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint32_t (&d)[kPrefixDw],
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+// The combined Toeplitz / CRC-32C byte tables (DESIGN.md "hash tables"),
+// staged in LDS: look(pos, b) = Toeplitz contribution (low word) and CRC
+// contribution (high word; only its low 9 bits reach the PCB bucket) of
+// tuple byte pos with value b.
+struct Tab64 {  // 12 x 256 u64 (24 KiB)
+  const uint64_t* T;
+  DEV uint64_t look(int pos, uint32_t b) const { return T[(pos << 8) | b]; }
+};
+struct TabSplit {  // 12 x 256 u32 Toeplitz + 12 x 256 u16 CRC (18 KiB)
+  const lds_u32* t32;
+  const lds_u16* t16;
+  DEV uint64_t look(int pos, uint32_t b) const {
+    return ((uint64_t)t16[(pos << 8) | b] << 32) | t32[(pos << 8) | b];
+  }
+};
+
+// Header shapes a wave can be specialised for (wave-uniform):
+// kShapeFixed: every lane IPv4 with ihl 5, the geometry constant-folded;
+// kShapeV4: every lane IPv4 (any ihl) or a non-IP frame, no IPv6 code;
+// kShapeV6: every lane IPv6 under IXG_F_IPV6 (L4 at the constant 54);
+// kShapeAny: anything.
+constexpr int kShapeFixed = 0, kShapeV4 = 1, kShapeV6 = 2, kShapeAny = 3;
+
+// NDW: prefix dwords available; a segment ending past 4*NDW bytes is left
+// to the streaming rounds.
+template <int SHAPE, int NDW, class Tab>
+DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixDw],
                     uint32_t L, LaneState& s, const lds_u32* T6 = nullptr) {
+  constexpr bool FIXED = SHAPE == kShapeFixed;
   const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);       // ip.c:132
   const uint32_t vh = byte_at(d, 14);
   const uint32_t ver = vh >> 4;
@@ -244,35 +281,79 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   const uint32_t src = (d[6] >> 16) | (d[7] << 16);                       // bytes 26..29 raw
   const uint32_t dst = (d[7] >> 16) | (d[8] << 16);                       // bytes 30..33 raw
   const int l4 = 14 + 4 * ihl;
-  const bool ip4 = etype == 0x0800u;
-  const bool v6 = !FIXED && etype == 0x86DDu && (p.flags & IXG_F_IPV6);
+  const bool ip4 = SHAPE != kShapeV6 && etype == 0x0800u;
+  const bool v6 = SHAPE == kShapeV6 || (SHAPE == kShapeAny && etype == 0x86DDu && (p.flags & IXG_F_IPV6));
 
   // L4 header dwords: frame byte l4+b sits in dword q + (2+b)/4, where
   // l4 = 4q + 2 (IPv4: q = 3 + max(ihl, 5); the IPv6 extension: L4 at 54,
-  // q = 13). The general shape reads them through a 4-stage mux.
+  // q = 13). The general shapes read them through a 4-stage mux.
   const int q = 3 + (ihl < 5 ? 5 : ihl);
   uint32_t h0, h1, h2, h3;
-  uint64_t C[kPrefixDw + 1];  // C[k] = sum of the 32-bit words of bytes [14, 4k)
-  uint64_t spre = 0;
+  // C[k] = one's complement (end-around carry) sum of the 32-bit words of
+  // bytes [14, 4k): congruent to the exact sum mod 2^32 - 1, and 0 only when
+  // every word is 0, so its 16-bit fold is the exact sum's. Half the registers
+  // and mux work of exact 64-bit sums. (General shapes only.)
+  uint32_t C[kPrefixDw + 1];
+  uint32_t spre = 0, reg32 = 0;
   if (FIXED) {
     h0 = d[8]; h1 = d[9]; h2 = d[10]; h3 = d[11];
   } else {
-    const uint32_t qs = v6 ? 5u : (uint32_t)(q - 8);  // in [0, 10]
-    uint32_t src4[kPrefixDw - 8], h[4];
-#pragma unroll
-    for (int j = 0; j < kPrefixDw - 8; j++) src4[j] = d[8 + j];
-    window<4>(src4, qs, h);
-    h0 = h[0]; h1 = h[1]; h2 = h[2]; h3 = h[3];
     C[3] = 0;
     C[4] = d[3] & 0xffff0000u;
 #pragma unroll
-    for (int k = 4; k < kPrefixDw; k++) C[k + 1] = C[k] + d[k];
-    // bytes [14, l4) = C[q] + the low half of dword q (= h0): the IPv4
-    // header, or the IPv6 header + the Ethernet type's successor bytes
-    uint64_t Cq[11];
+    for (int k = 4; k < kPrefixDw; k++) C[k + 1] = add1c(C[k], d[k]);
+    if (SHAPE == kShapeV6) {
+      h0 = d[13]; h1 = d[14]; h2 = d[15]; h3 = d[16];
+      spre = add1c(C[13], h0 & 0xffffu);
+    } else {
+      const uint32_t qs = v6 ? 5u : (uint32_t)(q - 8);  // in [0, 10]
+      uint32_t src4[kPrefixDw - 8], h[4];
 #pragma unroll
-    for (int j = 0; j < 11; j++) Cq[j] = C[8 + j];
-    spre = select<4>(Cq, qs) + (h0 & 0xffffu);
+      for (int j = 0; j < kPrefixDw - 8; j++) src4[j] = d[8 + j];
+      window<4>(src4, qs, h);
+      h0 = h[0]; h1 = h[1]; h2 = h[2]; h3 = h[3];
+      // bytes [14, l4) = C[q] + the low half of dword q (= h0): the IPv4
+      // header, or the IPv6 header + the Ethernet type's successor bytes
+      uint32_t Cq[11];
+#pragma unroll
+      for (int j = 0; j < 11; j++) Cq[j] = C[8 + j];
+      spre = add1c(select<4>(Cq, qs), h0 & 0xffffu);
+    }
+    // the L4 region's in-prefix sum, computed here while C[] is live (the
+    // hash lookups below then run without it)
+    {
+      static_assert(FIXED || NDW == kPrefixDw, "the general shapes sum the whole prefix");
+      const uint32_t se = v6 ? 54u + ((byte_at(d, 18) << 8) | byte_at(d, 19)) : 14u + ip_len;
+      const int e = (int)(se < (uint32_t)(4 * NDW) ? se : (uint32_t)(4 * NDW));
+      // bytes [l4, e) = [14, e) - [14, l4) (one's complement subtraction:
+      // add the complement); e >= l4 + 8 here (segments of at least 8
+      // bytes), so e's dword index is in [10, 24]
+      const uint32_t qe = (uint32_t)e >> 2;
+      const uint32_t qi = (qe < 10u ? 10u : qe) - 10u;
+      uint32_t Ce[15], de[15];
+#pragma unroll
+      for (int j = 0; j < 15; j++) {
+        Ce[j] = C[10 + j];
+        de[j] = 10 + j < kPrefixDw ? d[10 + j < kPrefixDw ? 10 + j : 0] : 0u;
+      }
+      const uint32_t s_e = add1c(select<4>(Ce, qi), select<4>(de, qi) & ones(e & 3));
+      uint32_t a32 = add1c(s_e, ~spre);
+      // x - x gives the negative zero 0xffffffff; it stands for an exact 0
+      // only when every byte of the region is 0 (the ICMP residual, which
+      // has no pseudo header, depends on the difference): rare, checked
+      // exactly, one mask per dword
+      if (wave_any(a32 == 0xffffffffu)) {
+        const int a = v6 ? 54 : l4;
+        uint32_t nz = 0;
+#pragma unroll
+        for (int j = 3; j < kPrefixDw; j++) {
+          const int lo = a - 4 * j, hi = e - 4 * j;
+          nz |= d[j] & keep_bytes(~0u, hi) & ~keep_bytes(~0u, lo);
+        }
+        if (a32 == 0xffffffffu && nz == 0) a32 = 0;
+      }
+      reg32 = a32;
+    }
   }
   const uint32_t b0 = (h0 >> 16) & 0xffu, b1 = h0 >> 24;                  // sport (wire)
   const uint32_t b2 = h1 & 0xffu, b3 = (h1 >> 8) & 0xffu;                 // dport (wire)
@@ -306,14 +387,14 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
   // ---- [NIC] RSS Toeplitz + tcp_to_idx via the byte tables ----
   const bool rss4 = hdr_ok && !frag && (proto == 6 || proto == 17) && (uint32_t)(l4 + 4) <= L;
   uint64_t hx = 0;
-  {
+  if (SHAPE != kShapeV6) {  // (IPv6 lanes use neither the v4 RSS nor the bucket)
     const uint32_t t4 = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
     uint32_t sb = src, db = dst, pb = t4;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      hx ^= T[(k << 8) | ((sb >> (8 * k)) & 0xffu)];
-      hx ^= T[((4 + k) << 8) | ((db >> (8 * k)) & 0xffu)];
-      hx ^= T[((8 + k) << 8) | ((pb >> (8 * k)) & 0xffu)];
+      hx ^= T.look(k, (sb >> (8 * k)) & 0xffu);
+      hx ^= T.look(4 + k, (db >> (8 * k)) & 0xffu);
+      hx ^= T.look(8 + k, (pb >> (8 * k)) & 0xffu);
     }
   }
   s.rss = 0;
@@ -321,25 +402,22 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
     s.rss = (uint32_t)hx;
     s.flags |= IXG_RF_RSS;
   }
-  // IPv6 extension: Toeplitz over src(16) dst(16) sport dport from the
-  // 36 x 256 table, staged in LDS by the general kernel
-  if (v6 && L >= 58 && ver == 6 && (s.proto == 6 || s.proto == 17)) {
+  // IPv6 extension: Toeplitz over src(16) dst(16) sport dport, one byte
+  // table lookup per tuple byte: positions 0..11 share the IPv4 tables' key
+  // offsets (their low words), positions 12..35 come from the IPv6 tables
+  // staged in LDS by the general kernels (IXG_TAB6_WORDS)
+  if (SHAPE != kShapeFixed && SHAPE != kShapeV4 && v6 && L >= 58 && ver == 6 && (s.proto == 6 || s.proto == 17)) {
     uint32_t h = 0;
 #pragma unroll
-    for (int k = 0; k < 32; k++) {
-      const uint32_t b = byte_at(d, 22 + k);
-      h ^= T6[(2 * k) * 16 + (b >> 4)] ^ T6[(2 * k + 1) * 16 + (b & 15u)];
-    }
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t b = byte_at(d, 54 + k);
-      h ^= T6[(2 * (32 + k)) * 16 + (b >> 4)] ^ T6[(2 * (32 + k) + 1) * 16 + (b & 15u)];
+    for (int k = 0; k < 36; k++) {
+      const uint32_t b = byte_at(d, k < 32 ? 22 + k : 54 + (k - 32));
+      h ^= k < 12 ? (uint32_t)T.look(k, b) : T6[((k - 12) << 8) | b];
     }
     s.rss = h;
     s.flags |= IXG_RF_RSS;
   }
   s.fg = p.fg_base + (s.rss & p.fg_mask);
-  s.bucket = ((uint32_t)(hx >> 32) ^ p.crc_const) & (IXG_PCB_BUCKETS - 1);
+  s.bucket = ((uint32_t)(hx >> 32) ^ p.crc_const) & (IXG_PCB_BUCKETS - 1);  // (9 bits of the CRC)
 
   // ---- L4 segment: [l4, 14 + ip_len) ----
   uint32_t l4len = ip_len - 4u * (uint32_t)ihl;
@@ -374,26 +452,13 @@ DEV void lane_parse(const KParams& p, const uint64_t* __restrict__ T, const uint
       for (int j = 0; j < NDW; j++) dd[j] = d[j];
       acc = region_sum(dd, 8, e);
     } else {
-      static_assert(FIXED || NDW == kPrefixDw, "the general shape sums the whole prefix");
-      // bytes [l4, e) = [14, e) - [14, l4); e >= l4 + 8 here
-      // (segments of at least 8 bytes), so e's dword index is in [10, 24]
-      const uint32_t qe = (uint32_t)e >> 2;
-      const uint32_t qi = (qe < 10u ? 10u : qe) - 10u;
-      uint64_t Ce[15];
-      uint32_t de[15];
-#pragma unroll
-      for (int j = 0; j < 15; j++) {
-        Ce[j] = C[10 + j];
-        de[j] = 10 + j < kPrefixDw ? d[10 + j < kPrefixDw ? 10 + j : 0] : 0u;
-      }
-      const uint64_t s_e = select<4>(Ce, qi) + (select<4>(de, qi) & ones(e & 3));
-      acc = s_e - spre;
+      acc = reg32;
     }
     if (kind == 1) {
       uint64_t ps;
       if (v6) {
         // src + dst: bytes [22, 54) = [14, 54) - [14, 22)
-        ps = (C[13] + (d[13] & 0xffffu)) - (C[5] + (d[5] & 0xffffu));
+        ps = add1c(add1c(C[13], d[13] & 0xffffu), ~add1c(C[5], d[5] & 0xffffu));
       } else {
         ps = (uint64_t)(src & 0xffffu) + (src >> 16) + (dst & 0xffffu) + (dst >> 16);
       }
@@ -508,8 +573,10 @@ DEV void store_record(const KParams& p, uint32_t i, const Rec& r, uint32_t ip_re
 // Fused PCB demux (ixg_rx_demux_batch_dev): the tcp_input lookup of an
 // IXG_V_TCP record straight from the parse state, no second pass over the
 // frames or the records (ixgrx_walk.h; dp/net/tcp_in.c:233-323, 500-510).
+// DMX false: a build without the fused demux (no lookup code in the kernel)
+template <bool DMX = true>
 DEV void store_demux(const KParams& p, uint32_t i, const Rec& r, uint32_t src, uint32_t dst, uint32_t ports) {
-  if (!p.dmx) return;
+  if (!DMX || !p.dmx) return;
   uint32_t id = 0, kind = IXG_D_NONE;
   if (((r.w0 >> 16) & 0xffu) == IXG_V_TCP) {
     const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
@@ -547,12 +614,6 @@ DEV void load_prefix(const uint8_t* f, uint32_t L, const uint8_t* dummy, uint32_
   }
 }
 
-// x & ones(clamp(t, 0, 4)): v_med3 + two shifts (the 64-bit one handles
-// the shift by 32) + v_bfi
-DEV uint32_t keep_bytes(uint32_t x, int t) {
-  const uint32_t u = (uint32_t)(t < 0 ? 0 : (t > 4 ? 4 : t));
-  return x & ~(uint32_t)(~0ull << (8u * u));
-}
 
 // Bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L"). Only the
 // dwords at or past the wave's shortest frame can hold such bytes: the
@@ -560,7 +621,7 @@ DEV uint32_t keep_bytes(uint32_t x, int t) {
 DEV void mask_prefix(uint32_t (&d)[kPrefixDw], uint32_t L) {
 #pragma unroll
   for (int j = 3; j < kPrefixDw; j++)
-    if (!__all(L >= 4u * (uint32_t)j + 4u)) d[j] = keep_bytes(d[j], (int)L - 4 * j);
+    if (!wave_all(L >= 4u * (uint32_t)j + 4u)) d[j] = keep_bytes(d[j], (int)L - 4 * j);
 }
 
 
@@ -568,7 +629,7 @@ DEV void mask_prefix(uint32_t (&d)[kPrefixDw], uint32_t L) {
 DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, bool valid, uint32_t L,
                       const uint32_t (&d)[kPrefixDw]) {
   LaneState s;
-  lane_parse<true, kFastDw>(p, T, d, L, s);
+  lane_parse<kShapeFixed, kFastDw>(p, Tab64{T}, d, L, s);
   if (valid) {
     const uint32_t r4 = l4_residual(s);
     const Rec r = make_record<true>(p, d, L, s, r4);
@@ -685,10 +746,10 @@ DEV void round_finish(const KParams& p, const WaveLds& w, int lane, const Round&
   a = add1c(a, a1);
   // frames longer than 96 + 2 KiB (not IX mbufs): the rest, synchronously
   const uint32_t more = kStreamBase + (16u << gsh) * kT;
-  if (__any(b.end > more)) {
+  if (wave_any(b.end > more)) {
     const uint64_t off = ((uint64_t)w.offhi[b.owner] << 32) | w.offlo[b.owner];
     const uint8_t* zero = p.zero + 16 * lane;
-    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 32u * gsz) {
+    for (uint32_t pos0 = more; wave_any(pos0 < b.end); pos0 += 32u * gsz) {
       const uint32_t pos = pos0 + 16u * gl;
       const u32x4 v0 = load16(pos < b.end, p.base + off + pos, zero);
       const u32x4 v1 = load16(pos + 16u * gsz < b.end, p.base + off + pos + 16u * gsz, zero);
@@ -736,7 +797,7 @@ DEV void gen_desc(const KParams& p, uint32_t chunk, int lane, GDesc& g) {
 // (a big chunk, see big_chunk, loads its prefixes in its rounds instead)
 template <bool GATE = false, bool BIG = false>
 DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
-  const bool skip = GATE ? !__all(g.L < IXG_SHORT_MAX) : (BIG && __all(g.L >= kBigMin || g.L == 0u));
+  const bool skip = GATE ? !wave_all(g.L < IXG_SHORT_MAX) : (BIG && wave_all(g.L >= kBigMin || g.L == 0u));
   const uint32_t Lg = skip ? 0u : g.L;
   load_prefix<0, 6>(p.base + g.off, Lg, reinterpret_cast<const uint8_t*>(p.tab), x.d);
   const bool short_tail = g.L > (uint32_t)kStreamBase && g.L < (uint32_t)kStreamBase + 32u;
@@ -797,11 +858,11 @@ DEV void big_finish(const KParams& p, const WaveLds& w, int lane, Round& b) {
   a = add1c(a, fold32((uint64_t)ve.x + ve.y + ve.z + ve.w));
   // frames longer than 2 KiB (not IX mbufs): the rest, synchronously
   const uint32_t more = 16u * kG * kT;
-  if (__any(b.end > more)) {
+  if (wave_any(b.end > more)) {
     const uint32_t owner = b.owner < 64u ? b.owner : 0u;
     const uint64_t off = ((uint64_t)w.offhi[owner] << 32) | w.offlo[owner];
     const uint8_t* zero = p.zero + 16 * lane;
-    for (uint32_t pos0 = more; __any(pos0 < b.end); pos0 += 16u * kG) {
+    for (uint32_t pos0 = more; wave_any(pos0 < b.end); pos0 += 16u * kG) {
       const uint32_t pos = pos0 + 16u * gl;
       // (b.ve did not load the end piece of such a frame)
       const u32x4 v = mask_piece(load16(pos < b.end, p.base + off + pos, zero), (int)b.end - (int)pos);
@@ -823,7 +884,7 @@ DEV uint32_t span_sum(const KParams& p, uint64_t off, uint32_t a, uint32_t e) {
   return fold32(s);
 }
 
-template <bool OFFS>
+template <bool OFFS, bool DMX = true>
 DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, const WaveLds& w,
                    const GDesc& g) {
   const uint32_t i = chunk * 64u + (uint32_t)lane;
@@ -855,10 +916,10 @@ DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t ch
   for (int j = 3; j < kPrefixDw; j++) d[j] = q[j];  // L >= 96: no masking
   LaneState s;
   const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
-  if (__all(fixed))
-    lane_parse<true, kPrefixDw>(p, T, d, L, s);
+  if (wave_all(fixed))
+    lane_parse<kShapeFixed, kPrefixDw>(p, Tab64{T}, d, L, s);
   else
-    lane_parse<false, kPrefixDw>(p, T, d, L, s, w.t6);
+    lane_parse<kShapeAny, kPrefixDw>(p, Tab64{T}, d, L, s, w.t6);
   if (!valid) return;
   uint32_t res = l4_residual(s);
   if (s.stream) {
@@ -867,7 +928,7 @@ DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t ch
   }
   const Rec r = make_record(p, d, L, s, res);
   store_record(p, i, r, s.ip_res, res);
-  store_demux(p, i, r, s.src, s.dst, s.ports);
+  store_demux<DMX>(p, i, r, s.src, s.dst, s.ports);
 }
 
 // MODE: kModeLong: any chunk; kModeFirst (the short kernel): the chunk's
@@ -882,7 +943,7 @@ constexpr int kModeLong = 0, kModeFirst = 2;
 // (Dn -> Pn) is loaded here, after this chunk's last streaming round is
 // issued (its registers free by then), instead of after this chunk, where
 // the next chunk waited out its whole latency
-template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false>
+template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false, bool DMX = true>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x, const GDesc* Dn = nullptr,
                        GPre* Pn = nullptr) {
@@ -891,12 +952,12 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   const bool valid = i < p.n;
   const uint32_t L = g.L;
   if (MODE == kModeFirst) {
-    const bool defer = !__all(L < IXG_SHORT_MAX);  // L = 0 past the end
+    const bool defer = !wave_all(L < IXG_SHORT_MAX);  // L = 0 past the end
     if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
     if (defer) return true;
   }
-  if (BIG && __all(g.L >= kBigMin || g.L == 0u)) {
-    big_chunk<OFFS>(p, T, chunk, lane, w, g);
+  if (BIG && wave_all(g.L >= kBigMin || g.L == 0u)) {
+    big_chunk<OFFS, DMX>(p, T, chunk, lane, w, g);
     if (LATE) gen_pre<false, BIG>(p, *Dn, lane, *Pn);
     return false;
   }
@@ -909,10 +970,10 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   const bool short_tail = L > (uint32_t)kStreamBase && L < (uint32_t)kStreamBase + 32u;
   LaneState s;
   const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
-  if (__all(fixed))
-    lane_parse<true, kPrefixDw>(p, T, d, L, s);
+  if (wave_all(fixed))
+    lane_parse<kShapeFixed, kPrefixDw>(p, Tab64{T}, d, L, s);
   else
-    lane_parse<false, kPrefixDw>(p, T, d, L, s, w.t6);
+    lane_parse<kShapeAny, kPrefixDw>(p, Tab64{T}, d, L, s, w.t6);
   // The 16-byte piece (counted from byte 96) holding the segment end is
   // summed by this lane, masked to the segment; streaming rounds read only
   // the whole pieces before it. A segment ending within 16 bytes past the
@@ -930,7 +991,7 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
       const uint32_t r4 = l4_residual(s);
       const Rec r = make_record(p, d, L, s, r4);
       store_record(p, i, r, s.ip_res, r4);
-      store_demux(p, i, r, s.src, s.dst, s.ports);
+      store_demux<DMX>(p, i, r, s.src, s.dst, s.ports);
     }
     return false;
   }
@@ -999,10 +1060,10 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
       const uint32_t end_piece = fold32(piece_sum(ve, (int)rr));
       const uint32_t res = (~fold16(add1c(add1c(acc32, w.sum[lane]), end_piece))) & 0xffffu;
       store_record(p, i, res == 0 ? rok : rbad, ip_res, res);
-      store_demux(p, i, res == 0 ? rok : rbad, tsrc, tdst, tports);
+      store_demux<DMX>(p, i, res == 0 ? rok : rbad, tsrc, tdst, tports);
     } else {
       store_record(p, i, rok, ip_res, r4);
-      store_demux(p, i, rok, tsrc, tdst, tports);
+      store_demux<DMX>(p, i, rok, tsrc, tdst, tports);
     }
   }
   return false;
@@ -1010,7 +1071,7 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
 
 // stage the hash tables (24 KiB) once per persistent workgroup
 DEV void stage_tables(const KParams& p, uint64_t* T) {
-  for (int k = threadIdx.x; k < 12 * 256 / 2; k += kBlock) {
+  for (int k = threadIdx.x; k < 12 * 256 / 2; k += blockDim.x) {
     const u32x4 v = reinterpret_cast<const u32x4*>(p.tab)[k];
     reinterpret_cast<u32x4*>(T)[k] = v;
   }
@@ -1047,7 +1108,7 @@ DEV void fetch_prefix(const KParams& p, uint32_t chunk, int lane, uint32_t L, ui
   // only frames that can be fast are worth loading; the bytes may run past
   // L into the next frame or the tail pad (include/ixgrx.h IXG_TAIL_PAD)
   // decided per wave: a chunk with any longer frame is deferred anyway
-  const bool ok = i < p.n && __all(L <= 64u || i >= p.n);
+  const bool ok = i < p.n && wave_all(L <= 64u || i >= p.n);
   const uint8_t* f = ok ? p.base + o : reinterpret_cast<const uint8_t*>(p.tab);
   x.w3 = *reinterpret_cast<const uint32_t*>(f + 12);
 #pragma unroll
@@ -1057,7 +1118,7 @@ DEV void fetch_prefix(const KParams& p, uint32_t chunk, int lane, uint32_t L, ui
 // a deferred chunk's class (ixgrx_internal.h): SHORT when no frame can need
 // the streaming rounds
 DEV uint32_t defer_class(bool valid, uint32_t L) {
-  return __all(!valid || L < IXG_SHORT_MAX) ? IXG_CLS_SHORT : IXG_CLS_LONG;
+  return wave_all(!valid || L < IXG_SHORT_MAX) ? IXG_CLS_SHORT : IXG_CLS_LONG;
 }
 
 // Publish the classes a wave deferred (bit k = class k): one store per wave
@@ -1096,7 +1157,7 @@ DEV uint32_t fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32
   const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
   const bool fast = !valid || (L <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
                                14 + ip_len <= 64);
-  const bool all_fast = __all(fast);
+  const bool all_fast = wave_all(fast);
   const uint32_t cls = all_fast ? 0u : defer_class(valid, L);
   if (lane == 0) p.defer[chunk] = (uint8_t)cls;
   if (!all_fast) return 1u << cls;
@@ -1284,7 +1345,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     // Bytes at offsets >= L read as zero. On this path nothing consumes a
     // byte >= L beyond offset 47 (the checksum regions end at or below L),
     // so frames with L >= 48 need no masking.
-    if (!__all(!valid || Lc >= 48u)) {
+    if (!wave_all(!valid || Lc >= 48u)) {
 #pragma unroll
       for (int j = 3; j < 16; j++) d[j] &= ones((int)Lc - 4 * j < 0 ? 0 : (int)Lc - 4 * j);
     }
@@ -1292,7 +1353,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
     const bool fast = !valid || (Lc <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
                                  14 + ip_len <= 64);
-    const bool all_fast = __all(fast);
+    const bool all_fast = wave_all(fast);
     const uint32_t cls = all_fast ? 0u : defer_class(valid, Lc);
     if (lane == 0) p.defer[c] = (uint8_t)cls;
     seen |= (1u << cls) & ~1u;
@@ -1301,7 +1362,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
       LaneState s;
       Rec r{0u, 0u, 0u, 0u};
       if (all_fast) {
-        lane_parse<true, kFastDw>(p, T, d, Lc, s);
+        lane_parse<kShapeFixed, kFastDw>(p, Tab64{T}, d, Lc, s);
         const uint32_t r4 = l4_residual(s);
         r = make_record<true>(p, d, Lc, s, r4);
         if (valid) store_record<true>(p, i, r, s.ip_res, r4);
@@ -1347,11 +1408,11 @@ ixg_rx_fastc_dmx_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false>
+template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false, bool BIG_OK = true, bool DMX = true>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
-  constexpr bool BIG = MODE == kModeLong && !EARLY;
+  constexpr bool BIG = BIG_OK && MODE == kModeLong && !EARLY;
   bool deferred = false;
   uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
   GDesc D1;
@@ -1365,7 +1426,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     GPre P1;
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     constexpr bool LATE = LATE_OK && !EARLY && MODE == kModeLong;
-    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE>(p, T, c0, lane, w, D0, P0, &D1, &P1);
+    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE, DMX>(p, T, c0, lane, w, D0, P0, &D1, &P1);
     if (!EARLY && !LATE) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
@@ -1381,7 +1442,8 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // fixed-shape kernel deferred as short or, in IXG_MODE_SHORT, walks every
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
-template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0, bool LATE = false>
+template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0, bool LATE = false, bool BIGOK = true,
+          int kWaves = 4, int kQGroups = 4, bool DMX = true>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -1389,7 +1451,8 @@ DEV void general_body(const KParams& p) {
   // the big-chunk prefix stash (not in the short kernel: no big chunks there)
   constexpr int kPre = CLS == IXG_CLS_SHORT ? 1 : 64 * kPrefixDw;
   __shared__ uint32_t sh_pre[kWaves][kPre];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // (the wave index is wave-uniform: kept in an SGPR)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
   const uint32_t ngroups = (nchunks + 63u) >> 6;
@@ -1412,10 +1475,10 @@ DEV void general_body(const KParams& p) {
     any = __ballot(ci < nchunks && mine(ci)) != 0;
   }
   if (!__syncthreads_or(any)) return;
-  // IPv6 Toeplitz nibble table (4.5 KiB, dynamic LDS: present only with IXG_F_IPV6)
+  // IPv6 Toeplitz tables (24 KiB, dynamic LDS: present only with IXG_F_IPV6)
   extern __shared__ u32x4 dyn6[];
   if (p.tab6) {
-    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += kBlock) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kWaves) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
   }
   stage_tables(p, T);
   const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
@@ -1445,11 +1508,11 @@ DEV void general_body(const KParams& p) {
     GDesc D0;
     gen_desc<OFFS>(p, q[0], lane, D0);
     if (CLS == IXG_CLS_SHORT)
-      seen |= gen_walk<OFFS, SEARLY, kModeFirst>(p, T, w, q, nq, lane, D0);
-    else if (__any(D0.L > (uint32_t)kStreamBase + 32u))
-      gen_walk<OFFS, false, kModeLong, SM, LATE>(p, T, w, q, nq, lane, D0);
+      seen |= gen_walk<OFFS, SEARLY, kModeFirst, 0, false, true, DMX>(p, T, w, q, nq, lane, D0);
+    else if (!SEARLY || wave_any(D0.L > (uint32_t)kStreamBase + 32u))
+      gen_walk<OFFS, false, kModeLong, SM, LATE, BIGOK, DMX>(p, T, w, q, nq, lane, D0);
     else
-      gen_walk<OFFS, true, kModeLong, SM>(p, T, w, q, nq, lane, D0);
+      gen_walk<OFFS, true, kModeLong, SM, false, true, DMX>(p, T, w, q, nq, lane, D0);
     __builtin_amdgcn_wave_barrier();
   }
   if (CLS == IXG_CLS_SHORT) publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
@@ -1457,6 +1520,12 @@ DEV void general_body(const KParams& p) {
 
 #define IXG_GEN_KERNEL(NAME, OFFS, CLS, WAVES, ...)                                                 \
   extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
+  NAME(KParams p) { general_body<OFFS, CLS, ##__VA_ARGS__>(p); }
+// Blocks of BW waves sharing one LDS copy of the hash tables (24 KiB, + the
+// IPv6 tables' 24 KiB under IXG_F_IPV6): two 10-wave blocks per CU give 5
+// waves per SIMD within LDS (2 x 58 KiB), 8-wave blocks 4.
+#define IXG_GENW_KERNEL(NAME, BW, OFFS, CLS, WAVES, ...)                                              \
+  extern "C" __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(WAVES)))  \
   NAME(KParams p) { general_body<OFFS, CLS, ##__VA_ARGS__>(p); }
 // behind the coalesced kernel (frames <= 64 B per stride, so deferred
 // chunks are nearly always short): one dispatch takes both classes, saving
@@ -1469,8 +1538,421 @@ IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
 // the short-class general kernel (no streaming rounds): 4 waves/SIMD
 // without the one-ahead prefix prefetch (128 VGPRs; C5 -3% against the
 // 3-wave prefetching build)
+// without the fused demux code and with it (4 waves/SIMD, 8-wave blocks;
+// the build without it at 5 waves/SIMD and 96 VGPRs, A/B variant w10, ran
+// C5 20% slower)
+IXG_GENW_KERNEL(ixg_rx_short_w8_s, 8, false, IXG_CLS_SHORT, 4, false, 0, false, true, 8, 4, false)
+IXG_GENW_KERNEL(ixg_rx_short_w8_o, 8, true, IXG_CLS_SHORT, 4, false, 0, false, true, 8, 4, false)
+IXG_GENW_KERNEL(ixg_rx_short_w8d_s, 8, false, IXG_CLS_SHORT, 4, false, 0, false, true, 8)
+IXG_GENW_KERNEL(ixg_rx_short_w8d_o, 8, true, IXG_CLS_SHORT, 4, false, 0, false, true, 8)
+
+// ---- the span-staged short kernel ------------------------------------------
+// Short chunks (every frame < IXG_SHORT_MAX bytes) whose frames lie in one
+// contiguous span of at most kSpanMax bytes (packed batches: the frames of a
+// chunk back to back; fixed strides <= 96 B) are staged through LDS: the
+// wave copies the span HBM -> LDS with global_load_lds_dwordx4 (1 KiB per
+// wave instruction, fully coalesced, no VGPRs), then each lane reads its own
+// frame's bytes 12..111 from LDS. Per-lane 16-byte loads of the prefixes
+// (the other kernels) touch 64 cache lines per instruction; measured on C5
+// the L1 spent most cycles stalled on their pending misses (TD busy 85 %,
+// TA stalled by TC). The copy of the wave's next chunk is issued as soon as
+// the current one has been read out of LDS, so it overlaps the parse.
+// Chunks that are not span-contiguous take per-lane loads.
+constexpr uint32_t kSpanMax = 6144;             // bytes per wave's span buffer
+constexpr int kSpanWaves = 16;                  // 1024-thread blocks, 1 per CU
+constexpr uint32_t kGldsWait = 0x0F70;          // s_waitcnt vmcnt(0) (gfx9 encoding)
+constexpr uint32_t kLdsWait = 0xC07F;           // s_waitcnt lgkmcnt(0)
+
+// A chunk's span: LDS image of [base, base + 1024 * npc) (npc = 0: not
+// span-contiguous, load per lane)
+struct Span {
+  uint64_t base;
+  uint32_t npc;
+};
+
+// Decide and issue the span copy of a chunk (descriptors g, wave-uniform
+// result). Every lane needs bytes [off, off + min(L, 112)).
+template <bool OFFS>
+DEV Span span_issue(const KParams& p, const GDesc& g, int lane, bool live, lds_u32* buf) {
+  Span sp{0, 0};
+  if (!live) return sp;
+  const uint32_t need = g.L < IXG_SHORT_MAX ? g.L : IXG_SHORT_MAX;
+  const uint64_t base = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)g.off) |
+                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(g.off >> 32)) << 32);
+  const uint64_t b16 = base & ~15ull;
+  const uint64_t end = g.off + need;
+  // the last lane's end bounds the span when the offsets ascend (packed)
+  const uint64_t e63 = (uint64_t)__builtin_amdgcn_readlane((uint32_t)end, 63) |
+                       ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(end >> 32), 63) << 32);
+  const bool ok = g.L == 0u || (g.off >= base && end <= e63 && e63 - b16 <= kSpanMax);
+  if (!wave_all(ok)) return sp;
+  sp.base = b16;
+  sp.npc = (uint32_t)((e63 - b16 + 1023u) >> 10);
+  const uint64_t top = e63 - b16;  // bytes of the span that exist (the rest: zero page)
+  for (uint32_t k = 0; k < sp.npc; k++) {
+    const uint32_t o = 1024u * k + 16u * (uint32_t)lane;
+    const uint8_t* src = o < top ? p.base + b16 + o : p.zero + 16 * lane;
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + 256u * k),
+                                     16, 0, 0);
+  }
+  return sp;
+}
+
+template <bool OFFS, bool DMX>
+DEV void short_span_body(const KParams& p) {
+  constexpr int W = kSpanWaves;
+  __shared__ uint64_t T[12 * 256];
+  // (+32 dwords: a lane reads up to 112 bytes from its frame start; the
+  // bytes past its frame are masked, but stay inside the buffer)
+  __shared__ uint32_t sh_span[W][kSpanMax / 4 + 32];
+  __shared__ uint32_t sh_q[W][64];
+  extern __shared__ u32x4 dyn6[];  // IPv6 Toeplitz tables (IXG_F_IPV6)
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * W;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t ngroups = (nchunks + 63u) >> 6;
+  const uint32_t mode = launch_mode(p);
+  const bool all = mode == IXG_MODE_SHORT;
+  if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
+  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
+  bool any = all;
+  for (uint32_t g = blockIdx.x * W + wave; !any && g < ngroups; g += nw) {
+    const uint32_t ci = g * 64u + (uint32_t)lane;
+    any = wave_any(ci < nchunks && mine(ci));
+  }
+  if (!__syncthreads_or(any)) return;
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * W)
+      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
+  stage_tables(p, T);
+  const Tab64 tab{T};
+  const lds_u32* t6 = LDS(const lds_u32, dyn6);
+  lds_u32* buf = LDS(lds_u32, sh_span[wave]);
+  lds_u32* q = LDS(lds_u32, sh_q[wave]);
+  bool seen = false;
+  for (uint32_t g0 = blockIdx.x * W + wave; g0 < ngroups; g0 += nw) {
+    const uint32_t ci = g0 * 64u + (uint32_t)lane;
+    const bool want = ci < nchunks && (all || mine(ci));
+    const uint64_t m = __ballot(want);
+    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+    const uint32_t nq = (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (nq == 0) continue;
+    // a chunk is live unless it holds a frame of IXG_SHORT_MAX bytes or more
+    // (then it is flagged for the long kernel here)
+    auto classify = [&](uint32_t chunk, GDesc& g) {
+      const bool defer = !wave_all(g.L < IXG_SHORT_MAX);  // (L = 0 past the batch end)
+      if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
+      seen |= defer;
+      if (defer) g.L = 0;
+      return !defer;
+    };
+    uint32_t c0 = q[0];
+    GDesc D0, D1;
+    gen_desc<OFFS>(p, c0, lane, D0);
+    bool live0 = classify(c0, D0);
+    Span S0 = span_issue<OFFS>(p, D0, lane, live0, buf);
+    uint32_t c1 = nq > 1 ? q[1] : kNoChunk;
+    gen_desc<OFFS>(p, c1, lane, D1);
+    for (uint32_t j = 0; j < nq; j++) {
+      const uint32_t i = c0 * 64u + (uint32_t)lane;
+      const bool valid = live0 && i < p.n;
+      const uint32_t L = D0.L;
+      uint32_t d[kPrefixDw];
+      u32x4 v96 = {0u, 0u, 0u, 0u};
+      if (S0.npc) {
+        __builtin_amdgcn_s_waitcnt(kGldsWait);
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t w0 = (uint32_t)(D0.off - S0.base) >> 2;
+        const lds_u32* f = buf + (L ? w0 : 0u);
+        d[0] = d[1] = d[2] = 0;
+#pragma unroll
+        for (int k = 3; k < kPrefixDw; k++) d[k] = f[k];
+        if (wave_any(L > (uint32_t)kStreamBase)) v96 = u32x4{f[24], f[25], f[26], f[27]};
+      } else {
+        GPre x;
+        gen_pre<false, false>(p, D0, lane, x);
+#pragma unroll
+        for (int k = 0; k < kPrefixDw; k++) d[k] = x.d[k];
+        v96 = x.v96;
+      }
+      // (every lane has its bytes: the next chunk's copy may overwrite the buffer)
+      __builtin_amdgcn_s_waitcnt(kLdsWait);
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t c2 = j + 2 < nq ? q[j + 2] : kNoChunk;
+      bool live1 = false;
+      Span S1{0, 0};
+      if (j + 1 < nq) {
+        live1 = classify(c1, D1);
+        S1 = span_issue<OFFS>(p, D1, lane, live1, buf);
+      }
+      GDesc D2;
+      gen_desc<OFFS>(p, c2, lane, D2);
+      // ---- parse chunk c0 ----
+      if (live0) {
+        mask_prefix(d, L);
+        LaneState st;
+        const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
+        if (wave_all(fixed))
+          lane_parse<kShapeFixed, kPrefixDw>(p, tab, d, L, st);
+        else
+          lane_parse<kShapeAny, kPrefixDw>(p, tab, d, L, st, t6);
+        // the 16-byte piece holding a segment end past byte 96 (frames < 112 B)
+        if (valid && st.stream) st.l4_acc += piece_sum(v96, (int)(st.seg_end - (uint32_t)kStreamBase));
+        if (valid) {
+          const uint32_t r4 = l4_residual(st);
+          const Rec r = make_record(p, d, L, st, r4);
+          store_record(p, i, r, st.ip_res, r4);
+          store_demux<DMX>(p, i, r, st.src, st.dst, st.ports);
+        }
+      }
+      c0 = c1;
+      c1 = c2;
+      D0 = D1;
+      D1 = D2;
+      live0 = live1;
+      S0 = S1;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
+}
+
+#define IXG_SPAN_KERNEL(NAME, OFFS, DMX)                                                                       \
+  extern "C" __global__ void __launch_bounds__(64 * kSpanWaves) __attribute__((amdgpu_waves_per_eu(4))) \
+  NAME(KParams p) { short_span_body<OFFS, DMX>(p); }
+IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
+IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
+#ifdef IXGRX_AB
+IXG_GENW_KERNEL(ixg_rx_short_w10_s, 10, false, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
+IXG_GENW_KERNEL(ixg_rx_short_w10_o, 10, true, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
+#endif
+#ifdef IXGRX_AB
 IXG_GEN_KERNEL(ixg_rx_short_late_s, false, IXG_CLS_SHORT, 4, false)
 IXG_GEN_KERNEL(ixg_rx_short_late_o, true, IXG_CLS_SHORT, 4, false)
+#endif
+
+// ---- the compacted short kernel (wavefront compaction across waves) ------
+// A block of kCxWaves waves takes a tile of kCxWaves short chunks (one per
+// wave) at a time. Phase 1: each lane loads its frame's prefix and classes
+// it: A = IPv4 ihl 5, C = other IPv4, B = IPv6 under IXG_F_IPV6, D = no IP
+// parse at all (ARP, other ethertypes, IPv6 in the reference's semantics:
+// ip.c:132-137), whose record is a constant of the ethertype and L and is
+// written at once. The A, C and B lanes are ranked by class across the
+// tile's waves (ballot + mbcnt + per-wave counts) and their prefixes written
+// to LDS in that order. Phase 2: the waves take the ranked list 64 entries at
+// a time, so nearly every wave holds one family and runs the parse
+// specialised for it (constant geometry for ihl 5 and for IPv6, no IPv6
+// code for IPv4). Only the waves straddling a class boundary run the
+// general parse. Records go to their frames' slots directly.
+constexpr int kCxWaves = 8;
+constexpr int kCxDw = 25;  // per ranked entry: bytes 16..111 (24 dwords) + meta
+constexpr uint32_t kClsA = 0, kClsC = 1, kClsB = 2, kClsD = 3, kClsNone = 4;
+
+struct __attribute__((aligned(16))) CxLds {
+  uint32_t t32[12 * 256];   // Toeplitz byte tables
+  uint16_t t16[12 * 256];   // CRC-32C byte tables (low 16 bits)
+  uint32_t x[kCxWaves * 64 * kCxDw];  // ranked prefixes
+  uint32_t cl[kCxWaves * 64];         // the block group's chunk list
+  uint32_t cnt[kCxWaves][4];          // per-wave counts (A, C, B; list fill)
+};
+
+// The record of a frame that eth_input never hands to ip_input: ARP
+// (ip.c:134-135) or a dropped ethertype (ip.c:136-137). No checksum is
+// checked, no RSS (fg = the device's group 0), no bucket.
+DEV Rec trivial_record(const KParams& p, uint32_t etype, uint32_t L) {
+  const bool arp = etype == 0x0806u;
+  Rec r;
+  r.w0 = p.fg_base | ((arp ? (uint32_t)IXG_V_ARP : (uint32_t)IXG_V_DROP_ETHERTYPE) << 16);
+  r.w1 = arp ? (14u | (((L >= 14 ? L - 14 : 0u) & 0xffffu) << 16)) : 0u;
+  r.w2 = 0;
+  r.w3 = IXG_NO_BUCKET;
+  return r;
+}
+
+// One ranked entry, parsed with the wave's shape: prefix from LDS, parse,
+// record, stores. A function per shape, called from a wave-uniform branch,
+// each reading its own copy of the entry (shared code hoisted above the
+// branch would stay live through every shape).
+template <int SHAPE>
+DEV void cx_entry(const KParams& p, const TabSplit& T, const lds_u32* t6, const lds_u32* e, uint32_t c2, bool ok,
+                  const lds_u32* CL, uint32_t t) {
+  uint32_t dd[kPrefixDw];
+  const uint32_t meta = e[24];
+  // bytes 12..13 (the ethertype) follow from the class
+  dd[0] = dd[1] = dd[2] = 0;
+  dd[3] = (c2 == kClsB ? 0xDD86u : 0x0008u) | (meta << 16);
+#pragma unroll
+  for (int j = 4; j < kPrefixDw; j++) dd[j] = e[j - 4];
+  const uint32_t Lx = (meta >> 16) & 0x7fu;
+  LaneState st;
+  lane_parse<SHAPE, kPrefixDw>(p, T, dd, Lx, st, t6);
+  // the 16-byte piece holding a segment end past byte 96 (frames < 112 B)
+  // and the frame's index, read only now (fewer registers live in the parse)
+  if (st.stream) {
+    const u32x4 v96 = {e[20], e[21], e[22], e[23]};
+    st.l4_acc += piece_sum(v96, (int)(st.seg_end - (uint32_t)kStreamBase));
+  }
+  if (ok) {
+    const uint32_t ti = e[24] >> 23;
+    const uint32_t ix = CL[t + (ti >> 6)] * 64u + (ti & 63u);
+    const uint32_t r4 = l4_residual(st);
+    const Rec r = make_record(p, dd, Lx, st, r4);
+    store_record(p, ix, r, st.ip_res, r4);
+    store_demux(p, ix, r, st.src, st.dst, st.ports);
+  }
+}
+
+// SHAPES: bit k = shape k may be used (A/B of the specialisations)
+template <bool OFFS, int SHAPES = 15>
+DEV void short_cx_body(const KParams& p) {
+  extern __shared__ u32x4 dyn6[];  // IPv6 Toeplitz tables (IXG_F_IPV6)
+  __shared__ CxLds sh;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t nbg = (nchunks + 64u * kCxWaves - 1u) / (64u * kCxWaves);  // block groups
+  const uint32_t mode = launch_mode(p);
+  const bool all = mode == IXG_MODE_SHORT;
+  if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
+  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
+  bool any = all;
+  for (uint32_t g = blockIdx.x * kCxWaves + wave; !any && g < nbg * kCxWaves; g += gridDim.x * kCxWaves) {
+    const uint32_t ci = g * 64u + (uint32_t)lane;
+    any = __ballot(ci < nchunks && mine(ci)) != 0;
+  }
+  if (!__syncthreads_or(any)) return;
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kCxWaves)
+      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
+  for (int k = threadIdx.x; k < 12 * 256 / 4; k += 64 * kCxWaves)
+    reinterpret_cast<u32x4*>(sh.t32)[k] = reinterpret_cast<const u32x4*>(p.tab32)[k];
+  for (int k = threadIdx.x; k < 12 * 256 / 8; k += 64 * kCxWaves)
+    reinterpret_cast<u32x4*>(sh.t16)[k] = reinterpret_cast<const u32x4*>(p.tab16)[k];
+  __syncthreads();
+  const TabSplit T{LDS(const lds_u32, sh.t32), LDS(const lds_u16, sh.t16)};
+  const lds_u32* t6 = LDS(const lds_u32, dyn6);
+  lds_u32* X = LDS(lds_u32, sh.x);
+  lds_u32* CL = LDS(lds_u32, sh.cl);
+  bool seen = false;
+  for (uint32_t bg = blockIdx.x; bg < nbg; bg += gridDim.x) {
+    // the block group's chunks (kCxWaves x 64), the short ones in order
+    {
+      const uint32_t ci = (bg * kCxWaves + wave) * 64u + (uint32_t)lane;
+      const bool want = ci < nchunks && (all || mine(ci));
+      const uint64_t m = __ballot(want);
+      if (lane == 0) sh.cnt[wave][3] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t base = 0;
+      for (int w = 0; w < wave; w++) base += sh.cnt[w][3];
+      if (want) CL[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+    }
+    __syncthreads();
+    uint32_t nq = 0;
+    for (int w = 0; w < kCxWaves; w++) nq += sh.cnt[w][3];
+    __syncthreads();  // (the counts are rewritten below)
+    for (uint32_t t = 0; t < nq; t += kCxWaves) {
+      // ---- phase 1: this wave's chunk ----
+      const uint32_t tc = t + (uint32_t)wave;
+      const uint32_t chunk = tc < nq ? CL[tc] : kNoChunk;
+      GDesc g;
+      gen_desc<OFFS>(p, chunk, lane, g);
+      bool live = chunk != kNoChunk;
+      if (live) {
+        const bool defer = !wave_all(g.L < IXG_SHORT_MAX);  // (g.L = 0 past the batch end)
+        if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
+        seen |= defer;
+        live = !defer;
+      }
+      if (!live) g.L = 0;  // (no frame bytes for a deferred chunk)
+      GPre x;
+      gen_pre<false, false>(p, g, lane, x);
+      const uint32_t i = chunk * 64u + (uint32_t)lane;
+      const bool valid = live && i < p.n;
+      const uint32_t L = g.L;
+      uint32_t d[kPrefixDw];
+#pragma unroll
+      for (int j = 0; j < kPrefixDw; j++) d[j] = x.d[j];
+      mask_prefix(d, L);
+      const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
+      uint32_t cls = kClsNone;
+      if (valid) {
+        if (etype == 0x0800u) cls = byte_at(d, 14) == 0x45u ? kClsA : kClsC;
+        else if (etype == 0x86DDu && (p.flags & IXG_F_IPV6)) cls = kClsB;
+        else cls = kClsD;
+      }
+      if (cls == kClsD) {
+        const Rec r = trivial_record(p, etype, L);
+        store_record(p, i, r, 0xffffu, 0xffffu);
+        store_demux(p, i, r, 0u, 0u, 0u);
+      }
+      const uint64_t mA = __ballot(cls == kClsA), mC = __ballot(cls == kClsC), mB = __ballot(cls == kClsB);
+      if (lane == 0) {
+        sh.cnt[wave][0] = (uint32_t)__popcll(mA);
+        sh.cnt[wave][1] = (uint32_t)__popcll(mC);
+        sh.cnt[wave][2] = (uint32_t)__popcll(mB);
+      }
+      __syncthreads();
+      uint32_t tot[3] = {0, 0, 0}, before[3] = {0, 0, 0};
+#pragma unroll
+      for (int w = 0; w < kCxWaves; w++) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+          const uint32_t c = sh.cnt[w][k];
+          tot[k] += c;
+          before[k] += w < wave ? c : 0u;
+        }
+      }
+      if (cls < kClsD) {
+        const uint64_t mm = cls == kClsA ? mA : (cls == kClsC ? mC : mB);
+        const uint32_t cbase = cls == kClsA ? 0u : (cls == kClsC ? tot[0] : tot[0] + tot[1]);
+        const uint32_t pos = cbase + (cls == kClsA ? before[0] : (cls == kClsC ? before[1] : before[2])) +
+                             __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
+        lds_u32* e = X + pos * kCxDw;
+#pragma unroll
+        for (int j = 4; j < kPrefixDw; j++) e[j - 4] = d[j];
+        e[20] = x.v96.x; e[21] = x.v96.y; e[22] = x.v96.z; e[23] = x.v96.w;
+        e[24] = (d[3] >> 16) | (L << 16) | ((uint32_t)(wave * 64 + lane) << 23);
+      }
+      __syncthreads();
+      // ---- phase 2: the ranked entries, 64 per wave ----
+      const uint32_t nA = tot[0], nAC = tot[0] + tot[1], nit = nAC + tot[2];
+      for (uint32_t k = (uint32_t)wave; 64u * k < nit; k += kCxWaves) {
+        const uint32_t pos = 64u * k + (uint32_t)lane;
+        const bool ok = pos < nit;
+        const lds_u32* e = X + (ok ? pos : 0u) * kCxDw;
+        const uint32_t c2 = pos < nA ? kClsA : (pos < nAC ? kClsC : kClsB);
+        const bool allA = wave_all(!ok || c2 == kClsA), allAC = wave_all(!ok || c2 != kClsB),
+                   allB = wave_all(!ok || c2 == kClsB);
+        if ((SHAPES & 1) && allA)
+          cx_entry<kShapeFixed>(p, T, t6, e, c2, ok, CL, t);
+        else if ((SHAPES & 2) && allAC)
+          cx_entry<kShapeV4>(p, T, t6, e, c2, ok, CL, t);
+        else if ((SHAPES & 4) && allB)
+          cx_entry<kShapeV6>(p, T, t6, e, c2, ok, CL, t);
+        else
+          cx_entry<kShapeAny>(p, T, t6, e, c2, ok, CL, t);
+      }
+      __syncthreads();  // X and the counts are reused by the next tile
+    }
+  }
+  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
+}
+
+#define IXG_CX_KERNEL(NAME, OFFS, ...)                                                                      \
+  extern "C" __global__ void __launch_bounds__(64 * kCxWaves) __attribute__((amdgpu_waves_per_eu(4))) \
+  NAME(KParams p) { short_cx_body<OFFS, ##__VA_ARGS__>(p); }
+#ifdef IXGRX_AB
+IXG_CX_KERNEL(ixg_rx_short_cx_s, false)
+IXG_CX_KERNEL(ixg_rx_short_cx_o, true)
+IXG_CX_KERNEL(ixg_rx_short_cx6_s, false, 4)
+IXG_CX_KERNEL(ixg_rx_short_cx6_o, true, 4)
+IXG_CX_KERNEL(ixg_rx_short_cx46_s, false, 6)
+IXG_CX_KERNEL(ixg_rx_short_cx46_o, true, 6)
+IXG_CX_KERNEL(ixg_rx_short_cx0_s, false, 0)
+IXG_CX_KERNEL(ixg_rx_short_cx0_o, true, 0)
+#endif
 #ifdef IXGRX_AB
 // A/B builds only (IXGRX_GEN_VARIANT / IXGRX_SHORT_VARIANT)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
@@ -1491,6 +1973,9 @@ IXG_GEN_KERNEL(ixg_rx_short_s, false, IXG_CLS_SHORT, 3)
 IXG_GEN_KERNEL(ixg_rx_short_o, true, IXG_CLS_SHORT, 3)
 IXG_GEN_KERNEL(ixg_rx_short_w4_s, false, IXG_CLS_SHORT, 4)
 IXG_GEN_KERNEL(ixg_rx_short_w4_o, true, IXG_CLS_SHORT, 4)
+// no big-chunk path, no one-ahead prefix: 3 waves/SIMD
+IXG_GEN_KERNEL(ixg_rx_general_w3nb_s, false, IXG_CLS_LONG, 3, false, 1, false, false)
+IXG_GEN_KERNEL(ixg_rx_general_w3nb_o, true, IXG_CLS_LONG, 3, false, 1, false, false)
 #endif
 
 // The sampler: one block reads the lengths of up to 64 evenly spread chunks
@@ -1509,8 +1994,8 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
     const uint32_t c = (uint32_t)((uint64_t)k * nchunks / ns);
     const uint32_t i = c * 64u + (uint32_t)lane;
     const uint32_t L = i < p.n ? p.len[i] : 0u;
-    nf += __all(L <= 64u) ? 1u : 0u;
-    nsh += __all(L < IXG_SHORT_MAX) ? 1u : 0u;
+    nf += wave_all(L <= 64u) ? 1u : 0u;
+    nsh += wave_all(L < IXG_SHORT_MAX) ? 1u : 0u;
   }
   if (lane == 0) {
     atomicAdd(&cnt[0], nf);
@@ -1541,13 +2026,27 @@ static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o}
                                    {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
                                    {ixg_rx_general_g16_s, ixg_rx_general_g16_o},
                                    {ixg_rx_general_pk_s, ixg_rx_general_pk_o},
-                                   {ixg_rx_general_lt_s, ixg_rx_general_lt_o}
+                                   {ixg_rx_general_lt_s, ixg_rx_general_lt_o},
+                                   {ixg_rx_general_w3nb_s, ixg_rx_general_w3nb_o}
 #endif
 };
-static const kern_fn k_short[][2] = {{ixg_rx_short_late_s, ixg_rx_short_late_o}
+// the short kernel (512-thread blocks by default)
+struct ShortK {
+  kern_fn k[2];
+  int block;
+};
+// with the fused demux (p.dmx)
+static const ShortK k_short_dmx = {{ixg_rx_short_w8d_s, ixg_rx_short_w8d_o}, 512};
+static const ShortK k_short[] = {{{ixg_rx_short_sp_s, ixg_rx_short_sp_o}, 64 * kSpanWaves}
 #ifdef IXGRX_AB
-                                     , {ixg_rx_short_w4_s, ixg_rx_short_w4_o},
-                                     {ixg_rx_short_s, ixg_rx_short_o}
+                                 , {{ixg_rx_short_w8_s, ixg_rx_short_w8_o}, 512}
+                                 , {{ixg_rx_short_w10_s, ixg_rx_short_w10_o}, 640}
+                                 , {{ixg_rx_short_late_s, ixg_rx_short_late_o}, kBlock},
+                                 {{ixg_rx_short_w4_s, ixg_rx_short_w4_o}, kBlock},
+                                 {{ixg_rx_short_s, ixg_rx_short_o}, kBlock},
+                                 {{ixg_rx_short_cx_s, ixg_rx_short_cx_o}, 64 * kCxWaves},
+                                 {{ixg_rx_short_cx6_s, ixg_rx_short_cx6_o}, 64 * kCxWaves},
+                                 {{ixg_rx_short_cx0_s, ixg_rx_short_cx0_o}, 64 * kCxWaves}
 #endif
 };
 static const int k_nshort = sizeof(k_short) / sizeof(k_short[0]);
@@ -1556,7 +2055,7 @@ static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
 
 // blocks per CU, cached per (kernel, dynamic LDS): a handful of entries,
 // filled under a lock (contexts on several host threads launch concurrently)
-static int occupancy(kern_fn k, size_t shmem) {
+static int occupancy(kern_fn k, size_t shmem, int block) {
   struct Entry { kern_fn k; size_t shmem; int nb; };
   static std::mutex mu;
   static Entry cache[32];
@@ -1565,13 +2064,13 @@ static int occupancy(kern_fn k, size_t shmem) {
   for (int i = 0; i < used; i++)
     if (cache[i].k == k && cache[i].shmem == shmem) return cache[i].nb;
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, kBlock, shmem) != hipSuccess || nb < 1) nb = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k, block, shmem) != hipSuccess || nb < 1) nb = 1;
   if (used < 32) cache[used++] = Entry{k, shmem, nb};
   return nb;
 }
 
-static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 0) {
-  const uint64_t cap = (uint64_t)ncu * (uint64_t)occupancy(k, shmem);
+static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 0, int block = kBlock) {
+  const uint64_t cap = (uint64_t)ncu * (uint64_t)occupancy(k, shmem, block);
   const uint64_t g = want < cap ? want : cap;
   return g ? (uint32_t)g : 1u;
 }
@@ -1619,8 +2118,13 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     return (int)hipGetLastError();
   }
   if (p.defer) {
-    const kern_fn ks = k_short[sv][lay];
-    hipLaunchKernelGGL(ks, dim3(grid_for(ks, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
+    const ShortK& ks = p.dmx ? k_short_dmx : k_short[sv];
+    // the general kernels: one wave per 64 chunks; the compacted A/B build:
+    // one block per 64 chunks per wave
+    const uint64_t ngroups = (nchunks + 63u) / 64u, bw = (uint64_t)ks.block / 64u;
+    const uint64_t want = (ngroups + bw - 1) / bw;
+    hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
+                       (hipStream_t)stream, p);
   }
   const kern_fn kg = k_gen[gv][lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);

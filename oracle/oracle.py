@@ -100,41 +100,70 @@ def rx_mbufs(key: bytes, nb: int, dev: int, flags: int, ptrs: np.ndarray, thread
 REF_HARNESS = os.path.join(_HERE, "_ref", "ixref_rx")
 
 
-def ref_time(tr, key: bytes, seconds: float, nb: int = 128, dev: int = 0, flags: int = 0,
-             max_frames: int = 65536):
-    """1-core rate of the reference's own RX code (oracle/_ref/ixref_rx,
-    built from /root/reference sources by `make -C oracle ref`) over the
-    first `max_frames` frames of `tr`, repeated for `seconds`. The harness
-    places each frame in a zeroed 2112-B IX mbuf and runs eth_input plus the
-    [NIC]-rule checksum/RSS calls, so it is an upper bound on the per-packet
-    cost of real IX (whose NIC does the checksums and RSS).
-    Returns (pkts/s, sample description) or (None, reason)."""
-    import json
+def _write_frames(path: str, tr, key: bytes, n: int, nb: int, dev: int, flags: int) -> None:
+    """The reference harnesses' frame file ("IXGRXIN1", harness_main.c)."""
     import struct
-    import tempfile
-    if not os.path.exists(REF_HARNESS):
-        return None, "oracle/_ref/ixref_rx not built"
-    n = min(max_frames, tr.n)
     offs = tr.offsets()[:n].astype(np.uint64)
     lens = tr.len[:n].astype(np.uint16)
     base = int(offs[0])
     end = int(offs[-1]) + int(lens[-1])
     blob = tr.blob[base:end]
     rel = (offs - base).astype(np.uint32)
+    with open(path, "wb") as f:
+        f.write(b"IXGRXIN1")
+        f.write(struct.pack("<IIHH", n, flags, nb, dev))
+        f.write(bytes(key))
+        f.write(lens.tobytes())
+        f.write(rel.tobytes())
+        f.write(struct.pack("<I", len(blob)))
+        f.write(blob.tobytes())
+
+
+def ref_time(tr, key: bytes, seconds: float, nb: int = 128, dev: int = 0, flags: int = 0,
+             max_frames: int = 65536):
+    """1-core rate of the reference harness (oracle/_ref/ixref_rx, built from
+    /root/reference sources by `make -C oracle ref`) over the first
+    `max_frames` frames of `tr`, repeated for `seconds`. The harness places
+    each frame in a zeroed 2112-B IX mbuf and runs eth_input plus the
+    [NIC]-rule checksum/RSS calls: harness overhead included, so not dp/ix's
+    own rate (ref_bench is). Returns (pkts/s, sample description) or (None, reason)."""
+    import json
+    import tempfile
+    if not os.path.exists(REF_HARNESS):
+        return None, "oracle/_ref/ixref_rx not built"
+    n = min(max_frames, tr.n)
     with tempfile.TemporaryDirectory() as d:
         fi, fo = os.path.join(d, "in"), os.path.join(d, "out")
-        with open(fi, "wb") as f:
-            f.write(b"IXGRXIN1")
-            f.write(struct.pack("<IIHH", n, flags, nb, dev))
-            f.write(bytes(key))
-            f.write(lens.tobytes())
-            f.write(rel.tobytes())
-            f.write(struct.pack("<I", len(blob)))
-            f.write(blob.tobytes())
+        _write_frames(fi, tr, key, n, nb, dev, flags)
         r = subprocess.run([REF_HARNESS, "-t", str(seconds), fi, fo], check=True, capture_output=True, text=True)
     d = json.loads(r.stdout.strip().splitlines()[-1])
     return 1e9 / d["ns_per_pkt"], f"oracle/_ref/ixref_rx (reference dp/net + dp/lwip objects) over {n} frames x " \
                                   f"{d['pkts'] // n} passes in {d['seconds']:.1f}s, 1 core"
+
+
+REF_BENCH = os.path.join(_HERE, "_ref", "ixref_bench")
+
+
+def ref_bench(tr, key: bytes, mode: str, procs: int, seconds: float, mbufs_per_proc: int = 1 << 16,
+              nb: int = 128, dev: int = 0, max_frames: int = 1 << 16):
+    """dp/ix's own RX path on `procs` host cores (oracle/_ref/ixref_bench,
+    harness_bench.c: the reference's eth_input -> ip_input -> tcp_input_tmp
+    -> tcp_input head with tcp_to_idx over pre-filled IX mbufs; mode "full"
+    adds the reference's checksum and Toeplitz functions, the NIC's work).
+    Returns the harness's JSON dict, or None when the binary is not built."""
+    import json
+    import tempfile
+    if not os.path.exists(REF_BENCH):
+        return None
+    n = min(max_frames, tr.n)
+    with tempfile.TemporaryDirectory() as d:
+        fi = os.path.join(d, "in")
+        _write_frames(fi, tr, key, n, nb, dev, 0)
+        r = subprocess.run([REF_BENCH, mode, str(procs), str(seconds), str(mbufs_per_proc), fi], check=True,
+                           capture_output=True, text=True, timeout=seconds + 120)
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    out["frames"] = n
+    return out
 
 
 class _DemuxTables(ctypes.Structure):
