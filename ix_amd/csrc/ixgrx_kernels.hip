@@ -266,9 +266,9 @@ constexpr int kShapeFixed = 0, kShapeV4 = 1, kShapeV6 = 2, kShapeAny = 3;
 
 // NDW: prefix dwords available; a segment ending past 4*NDW bytes is left
 // to the streaming rounds.
-template <int SHAPE, int NDW, class Tab>
+template <int SHAPE, int NDW, class Tab, class T6P = const lds_u32*>
 DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixDw],
-                    uint32_t L, LaneState& s, const lds_u32* T6 = nullptr) {
+                    uint32_t L, LaneState& s, T6P T6 = nullptr) {
   constexpr bool FIXED = SHAPE == kShapeFixed;
   const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);       // ip.c:132
   const uint32_t vh = byte_at(d, 14);
@@ -1249,8 +1249,12 @@ DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t l
   const uint64_t cbase = (uint64_t)cc * 64u * p.stride;
   const bool live = cc < nchunks;
   const uint8_t* cb = live ? p.base + cbase : p.zero;
+  // the chunk's own 64 * stride bytes only (pieces past them re-read the
+  // last one: no extra traffic); a frame reaching past its chunk (L > stride
+  // in lane 63) is not fixed-shape
   const uint64_t room = live ? lim - cbase - 16u : 4096u - 16u;
-  const uint32_t top = room < 4096u - 16u ? (uint32_t)room : 4096u - 16u;
+  const uint32_t cap = 64u * p.stride - 16u;
+  const uint32_t top = room < cap ? (uint32_t)room : cap;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t o = 16u * (uint32_t)(lane + 64 * k);
@@ -1305,13 +1309,45 @@ DEV void dmx_finish(const KParams& p, const PendDmx& q) {
   reinterpret_cast<u32x2v*>(p.dmx)[q.i] = u32x2v{id, kind};
 }
 
+// A chunk the coalesced kernel could not take as fixed-shape, finished by
+// the same wave after its fixed-shape chunks (no second dispatch): per-lane
+// prefix loads, the general parse, and a lane-serial sum of any segment
+// tail past byte 96 (coalesced batches have strides <= 64 B, so such tails
+// only come from frames reaching into the following slots: rare). The IPv6
+// tables, when in use, are read from global memory (rare path: no LDS).
 template <bool DMX>
+DEV void slow_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane) {
+  GDesc g;
+  gen_desc<false>(p, chunk, lane, g);
+  GPre x;
+  gen_pre<false, false>(p, g, lane, x);
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t L = g.L;
+  uint32_t d[kPrefixDw];
+#pragma unroll
+  for (int k = 0; k < kPrefixDw; k++) d[k] = x.d[k];
+  mask_prefix(d, L);
+  LaneState s;
+  lane_parse<kShapeAny, kPrefixDw>(p, Tab64{T}, d, L, s, p.tab6);
+  if (!valid) return;
+  uint32_t res = l4_residual(s);
+  if (s.stream) res = (~fold16(add1c(fold32(s.l4_acc), span_sum(p, g.off, (uint32_t)kStreamBase, s.seg_end)))) & 0xffffu;
+  const Rec r = make_record(p, d, L, s, res);
+  store_record(p, i, r, s.ip_res, res);
+  store_demux<DMX>(p, i, r, s.src, s.dst, s.ports);
+}
+
+template <bool DMX, bool DRAIN = true>
 DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* buf) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
   uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (c >= nchunks) return;
+  const uint32_t c_first = c;
+  uint64_t dmask = 0;  // bit k: the wave's k-th chunk was not fixed-shape
+  uint32_t kth = 0;
   // readable bytes: up to IXG_TAIL_PAD past the last frame's end
   const uint64_t lim = (uint64_t)(p.n - 1) * p.stride + p.len[p.n - 1] + IXG_TAIL_PAD;
   const uint32_t fw = (uint32_t)lane * (p.stride >> 2);  // this lane's frame, in dwords
@@ -1352,11 +1388,17 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
     const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
     const bool fast = !valid || (Lc <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
-                                 14 + ip_len <= 64);
+                                 14 + ip_len <= 64 && (lane != 63 || Lc <= p.stride));
     const bool all_fast = wave_all(fast);
+    // chunks that are not fixed-shape are finished after the loop (DRAIN)
+    // or flagged for the general kernels
     const uint32_t cls = all_fast ? 0u : defer_class(valid, Lc);
-    if (lane == 0) p.defer[c] = (uint8_t)cls;
-    seen |= (1u << cls) & ~1u;
+    if (!DRAIN || kth >= 64u) {
+      if (lane == 0) p.defer[c] = (uint8_t)cls;
+      seen |= (1u << cls) & ~1u;
+    }
+    if (DRAIN && kth < 64u && !all_fast) dmask |= 1ull << kth;
+    kth++;
     if (DMX) {
       // (a deferred chunk's records and demux records are the general kernel's)
       LaneState s;
@@ -1383,6 +1425,11 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   }
   if (DMX) dmx_finish(p, pend);
   publish_classes(p, seen, lane);
+  if (DRAIN) {
+    // the wave's own deferred chunks (its first 64: a wave has ~8; the rest,
+    // if any, were flagged for the general kernels above)
+    for (uint64_t m = dmask; m; m &= m - 1) slow_chunk<DMX>(p, T, c_first + (uint32_t)__builtin_ctzll(m) * nw, lane);
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
@@ -1527,10 +1574,6 @@ DEV void general_body(const KParams& p) {
 #define IXG_GENW_KERNEL(NAME, BW, OFFS, CLS, WAVES, ...)                                              \
   extern "C" __global__ void __launch_bounds__(64 * BW) __attribute__((amdgpu_waves_per_eu(WAVES)))  \
   NAME(KParams p) { general_body<OFFS, CLS, ##__VA_ARGS__>(p); }
-// behind the coalesced kernel (frames <= 64 B per stride, so deferred
-// chunks are nearly always short): one dispatch takes both classes, saving
-// the empty short dispatch on C2
-IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
 // (the default streams medium segments with 4-lane groups: C3 -5.5% in
 // A/B, and C3's FETCH_SIZE 6.64 -> 6.53 GB)
 IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
@@ -1572,7 +1615,7 @@ struct Span {
 
 // Decide and issue the span copy of a chunk (descriptors g, wave-uniform
 // result). Every lane needs bytes [off, off + min(L, 112)).
-template <bool OFFS>
+template <bool OFFS, int AUX = 0>
 DEV Span span_issue(const KParams& p, const GDesc& g, int lane, bool live, lds_u32* buf) {
   Span sp{0, 0};
   if (!live) return sp;
@@ -1593,12 +1636,13 @@ DEV Span span_issue(const KParams& p, const GDesc& g, int lane, bool live, lds_u
     const uint32_t o = 1024u * k + 16u * (uint32_t)lane;
     const uint8_t* src = o < top ? p.base + b16 + o : p.zero + 16 * lane;
     __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + 256u * k),
-                                     16, 0, 0);
+                                     16, 0, AUX);
   }
   return sp;
 }
 
-template <bool OFFS, bool DMX>
+// AUX: the copies' cache policy (2 = nt)
+template <bool OFFS, bool DMX, int AUX = 0, bool STRIDED = true>
 DEV void short_span_body(const KParams& p) {
   constexpr int W = kSpanWaves;
   __shared__ uint64_t T[12 * 256];
@@ -1616,9 +1660,13 @@ DEV void short_span_body(const KParams& p) {
   if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
   auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
   bool any = all;
-  for (uint32_t g = blockIdx.x * W + wave; !any && g < ngroups; g += nw) {
-    const uint32_t ci = g * 64u + (uint32_t)lane;
-    any = wave_any(ci < nchunks && mine(ci));
+  {
+    const uint32_t wv0 = blockIdx.x * W + wave;
+    for (uint32_t g = STRIDED ? 0u : wv0; !any && (STRIDED ? wv0 + 64u * g * nw < nchunks : g < ngroups);
+         g += STRIDED ? 1u : nw) {
+      const uint32_t ci = STRIDED ? wv0 + (64u * g + (uint32_t)lane) * nw : g * 64u + (uint32_t)lane;
+      any = wave_any(ci < nchunks && mine(ci));
+    }
   }
   if (!__syncthreads_or(any)) return;
   if (p.tab6) {
@@ -1631,8 +1679,14 @@ DEV void short_span_body(const KParams& p) {
   lds_u32* buf = LDS(lds_u32, sh_span[wave]);
   lds_u32* q = LDS(lds_u32, sh_q[wave]);
   bool seen = false;
-  for (uint32_t g0 = blockIdx.x * W + wave; g0 < ngroups; g0 += nw) {
-    const uint32_t ci = g0 * 64u + (uint32_t)lane;
+  // chunk assignment (STRIDED): wave wv takes chunks wv, wv + nw, wv + 2 nw, ...,
+  // so at any moment the grid reads one contiguous window of the batch (a
+  // wave per chunk) rather than one region per wave; else wave g takes the
+  // 64 consecutive chunks of group g
+  const uint32_t wv = blockIdx.x * W + wave;
+  for (uint32_t g0 = STRIDED ? 0u : wv; STRIDED ? wv + 64u * g0 * nw < nchunks : g0 < ngroups;
+       g0 += STRIDED ? 1u : nw) {
+    const uint32_t ci = STRIDED ? wv + (64u * g0 + (uint32_t)lane) * nw : g0 * 64u + (uint32_t)lane;
     const bool want = ci < nchunks && (all || mine(ci));
     const uint64_t m = __ballot(want);
     if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
@@ -1652,7 +1706,7 @@ DEV void short_span_body(const KParams& p) {
     GDesc D0, D1;
     gen_desc<OFFS>(p, c0, lane, D0);
     bool live0 = classify(c0, D0);
-    Span S0 = span_issue<OFFS>(p, D0, lane, live0, buf);
+    Span S0 = span_issue<OFFS, AUX>(p, D0, lane, live0, buf);
     uint32_t c1 = nq > 1 ? q[1] : kNoChunk;
     gen_desc<OFFS>(p, c1, lane, D1);
     for (uint32_t j = 0; j < nq; j++) {
@@ -1685,7 +1739,7 @@ DEV void short_span_body(const KParams& p) {
       Span S1{0, 0};
       if (j + 1 < nq) {
         live1 = classify(c1, D1);
-        S1 = span_issue<OFFS>(p, D1, lane, live1, buf);
+        S1 = span_issue<OFFS, AUX>(p, D1, lane, live1, buf);
       }
       GDesc D2;
       gen_desc<OFFS>(p, c2, lane, D2);
@@ -1719,11 +1773,15 @@ DEV void short_span_body(const KParams& p) {
   publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
 }
 
-#define IXG_SPAN_KERNEL(NAME, OFFS, DMX)                                                                       \
+#define IXG_SPAN_KERNEL(NAME, OFFS, DMX, ...)                                                                  \
   extern "C" __global__ void __launch_bounds__(64 * kSpanWaves) __attribute__((amdgpu_waves_per_eu(4))) \
-  NAME(KParams p) { short_span_body<OFFS, DMX>(p); }
+  NAME(KParams p) { short_span_body<OFFS, DMX, ##__VA_ARGS__>(p); }
 IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
 IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
+#ifdef IXGRX_AB
+IXG_SPAN_KERNEL(ixg_rx_short_spnt_s, false, false, 0, false)
+IXG_SPAN_KERNEL(ixg_rx_short_spnt_o, true, false, 0, false)
+#endif
 #ifdef IXGRX_AB
 IXG_GENW_KERNEL(ixg_rx_short_w10_s, 10, false, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
 IXG_GENW_KERNEL(ixg_rx_short_w10_o, 10, true, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
@@ -1955,6 +2013,9 @@ IXG_CX_KERNEL(ixg_rx_short_cx0_o, true, 0)
 #endif
 #ifdef IXGRX_AB
 // A/B builds only (IXGRX_GEN_VARIANT / IXGRX_SHORT_VARIANT)
+// round 1's second dispatch behind the coalesced kernel (both classes); the
+// coalesced kernel now finishes its deferred chunks itself
+IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
 IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
 IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
@@ -2039,7 +2100,8 @@ struct ShortK {
 static const ShortK k_short_dmx = {{ixg_rx_short_w8d_s, ixg_rx_short_w8d_o}, 512};
 static const ShortK k_short[] = {{{ixg_rx_short_sp_s, ixg_rx_short_sp_o}, 64 * kSpanWaves}
 #ifdef IXGRX_AB
-                                 , {{ixg_rx_short_w8_s, ixg_rx_short_w8_o}, 512}
+                                 , {{ixg_rx_short_w8_s, ixg_rx_short_w8_o}, 512},
+                                 {{ixg_rx_short_spnt_s, ixg_rx_short_spnt_o}, 64 * kSpanWaves}
                                  , {{ixg_rx_short_w10_s, ixg_rx_short_w10_o}, 640}
                                  , {{ixg_rx_short_late_s, ixg_rx_short_late_o}, kBlock},
                                  {{ixg_rx_short_w4_s, ixg_rx_short_w4_o}, kBlock},
@@ -2107,16 +2169,20 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     }
     // the coalesced kernel runs 8 resident-grids' worth of blocks (each wave
     // ~8 chunks): 3-4% faster on C2 than one persistent grid (A/B of 1x, 2x,
-    // 3x, 4x, 8x and one chunk per wave, which loses the prefetch: -30%)
-    const uint32_t gcu = (kf == ixg_rx_fastc_s || kf == ixg_rx_fastc_dmx_s) ? 8u * ncu : ncu;
-    if (kf) hipLaunchKernelGGL(kf, dim3(grid_for(kf, wave_blocks, gcu)), dim3(kBlock), 0, (hipStream_t)stream, p);
+    // 3x, 4x, 8x and one chunk per wave, which loses the prefetch: -30%); at
+    // least one block per 64 chunks per wave, so every wave can finish its
+    // own deferred chunks (fastc_loop's DRAIN)
+    const bool fc = kf == ixg_rx_fastc_s || kf == ixg_rx_fastc_dmx_s;
+    const uint32_t gcu = fc ? 8u * ncu : ncu;
+    if (kf) {
+      uint64_t gb = grid_for(kf, wave_blocks, gcu);
+      if (fc && gb < (nchunks + 64u * kWaves - 1) / (64u * kWaves)) gb = (nchunks + 64u * kWaves - 1) / (64u * kWaves);
+      hipLaunchKernelGGL(kf, dim3((uint32_t)gb), dim3(kBlock), 0, (hipStream_t)stream, p);
+    }
   }
-  const bool coal_any = p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0;
-  if (coal_any) {
-    hipLaunchKernelGGL(ixg_rx_any_s, dim3(grid_for(ixg_rx_any_s, group_blocks, ncu, sh6)), dim3(kBlock), sh6,
-                       (hipStream_t)stream, p);
-    return (int)hipGetLastError();
-  }
+  // coalesced batches in the default split: the coalesced kernel finished
+  // every chunk itself
+  if (p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0) return (int)hipGetLastError();
   if (p.defer) {
     const ShortK& ks = p.dmx ? k_short_dmx : k_short[sv];
     // the general kernels: one wave per 64 chunks; the compacted A/B build:
