@@ -41,6 +41,8 @@ extern "C" {
 
 /* Constants of the reference this ABI is bit-exact against. */
 #define IXG_ETH_MAX_NUM_FG 512u    /* inc/ix/ethfg.h:38 ETH_MAX_NUM_FG */
+#define IXG_ETH_MAX_TOTAL_FG 8192u /* inc/ix/ethfg.h:40-41 ETH_MAX_NUM_FG * NETHDEV (16): the
+                                      outbound flow groups follow, one per CPU (:135-138) */
 #define IXG_PCB_BUCKETS 512u       /* inc/ix/ethfg.h:42 TCP_ACTIVE_PCBS_MAX_BUCKETS */
 #define IXG_PCB_HASH_SEED 0xa36bdcbeu /* inc/lwip/lwip/tcp_impl.h:371 */
 #define IXG_MBUF_HEADER_LEN 64u    /* inc/ix/mbuf.h MBUF_HEADER_LEN: data at mbuf+64 */
@@ -112,11 +114,14 @@ enum ixg_verdict {
 #define IXG_RF_L4_CSUM_CHECKED 0x04u
 #define IXG_RF_L4_CSUM_OK 0x08u
 #define IXG_RF_RSS 0x10u /* rss_hash was computed (non-fragmented IPv4 TCP/UDP) */
+#define IXG_RF_FDIR 0x20u /* matched a flow-director perfect filter (ixg_rx_set_fdir): fg_id is
+                             the CPU's outbound flow group, not the RSS group */
 
 #define IXG_NO_BUCKET 0xffffu
 
 struct ixg_rx_rec {
-	uint16_t fg_id;      /* dev_idx*512 + (rss_hash & (nb_rx_fgs-1)) (ixgbe.c:329-335) */
+	uint16_t fg_id;      /* dev_idx*512 + (rss_hash & (nb_rx_fgs-1)) (ixgbe.c:329-335), or with
+	                        IXG_RF_FDIR the outbound group ETH_MAX_TOTAL_FG + cpu_id */
 	uint8_t verdict;     /* enum ixg_verdict */
 	uint8_t flags;       /* IXG_RF_* */
 	uint16_t l4_off;     /* payload offset from the frame start (see verdicts) */
@@ -178,6 +183,30 @@ int ixg_rx_hash_tables(const struct ixg_rx_cfg *cfg, uint64_t *tab12x256, uint32
 
 int ixg_abi_version(void);
 const char *ixg_strerror(int err);
+
+/* ---- flow director: the outbound connections' perfect filters ---------- */
+
+/* One perfect filter as get_port_with_fdir installs it for an outbound
+ * (bsys_tcp_connect) connection (dp/net/tcp_api.c:630-643): IPv4 TCP frames
+ * from the connection's remote address/port (src) to its local address/port
+ * (dst). */
+struct ixg_fdir_filter {
+	uint32_t src_ip;   /* raw, network byte order (frame bytes 26..29) */
+	uint32_t dst_ip;   /* raw (frame bytes 30..33) */
+	uint16_t src_port; /* host order */
+	uint16_t dst_port; /* host order */
+};
+
+/* Replace the context's filter set (n = 0: none, the default; IX removes
+ * them one by one, remove_fdir_filter tcp_api.c:606-619). A non-fragmented
+ * IPv4 TCP frame whose 4-tuple equals a filter's gets the NIC's FLM status:
+ * the driver sets fg_id = MBUF_INVALID_FG_ID (dp/drivers/ixgbe.c:329-330,
+ * i40e.c:380-381), which eth_recv_handle_fg_transition turns into
+ * outbound_fg_idx() = ETH_MAX_TOTAL_FG + cpu_id (dp/core/ethfg.c:502-505,
+ * inc/ix/ethfg.h:135-138). The record carries that fg_id and IXG_RF_FDIR;
+ * everything else about the frame is unchanged. cpu_id: the IX CPU the
+ * filters steer to (the queue of the CPU that connected). 0 or -errno. */
+int ixg_rx_set_fdir(void *ctx, const struct ixg_fdir_filter *filters, uint32_t n, uint16_t cpu_id);
 
 /* How the context's RX launches divide a batch between the kernels
  * (DESIGN.md 4.1). AUTO, the default, is the only setting a drop-in needs:

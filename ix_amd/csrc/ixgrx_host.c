@@ -92,6 +92,9 @@ struct ixg_ctx {
 	/* event emission scratch: per-chunk counts / bases */
 	uint32_t *d_evbase;
 	size_t evbase_cap;
+	/* flow-director perfect filters (ixg_rx_set_fdir) */
+	uint32_t *d_fdir;
+	uint32_t fdir_mask, fdir_fg;
 };
 
 /* ---- hash tables -------------------------------------------------------- */
@@ -227,6 +230,7 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_txsegs);
 	hipFree(c->d_txlen);
 	hipFree(c->d_evbase);
+	hipFree(c->d_fdir);
 	hipFree(c->d_frames);
 	hipFree(c->d_off);
 	hipFree(c->d_len);
@@ -356,6 +360,9 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
 	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
 	p.zero = c->d_zero;
+	p.fdir = c->d_fdir;
+	p.fdir_mask = c->fdir_mask;
+	p.fdir_fg = c->fdir_fg;
 	if (dmx) {
 		p.dmx = dmx;
 		p.active_start = c->d_astart;
@@ -386,6 +393,50 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 		p.force_mode = c->force_mode;
 	}
 	return ixgrx_launch(&p, c->variant, c->ncu, s) == 0 ? 0 : -EIO;
+}
+
+int ixg_rx_set_fdir(void *vctx, const struct ixg_fdir_filter *f, uint32_t n, uint16_t cpu_id)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && !f) || n > (1u << 24) || IXG_ETH_MAX_TOTAL_FG + (uint32_t)cpu_id > 0xfffeu)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	hipFree(c->d_fdir);
+	c->d_fdir = NULL;
+	c->fdir_mask = 0;
+	if (n == 0)
+		return 0;
+	/* open addressing, load factor <= 1/2, linear probing; duplicates kept
+	 * once (a perfect filter matches or not) */
+	uint32_t slots = 16;
+	while (slots < 2 * n)
+		slots <<= 1;
+	uint32_t *tab = (uint32_t *)calloc((size_t)slots * 4, sizeof(uint32_t));
+	if (!tab)
+		return -ENOMEM;
+	for (uint32_t i = 0; i < n; i++) {
+		const uint32_t ports = (uint32_t)f[i].src_port | ((uint32_t)f[i].dst_port << 16);
+		uint32_t k = ixg_fdir_hash(f[i].src_ip, f[i].dst_ip, ports) & (slots - 1);
+		while (tab[4 * k + 3] && !(tab[4 * k] == f[i].src_ip && tab[4 * k + 1] == f[i].dst_ip && tab[4 * k + 2] == ports))
+			k = (k + 1) & (slots - 1);
+		tab[4 * k] = f[i].src_ip;
+		tab[4 * k + 1] = f[i].dst_ip;
+		tab[4 * k + 2] = ports;
+		tab[4 * k + 3] = 1;
+	}
+	int rc = 0;
+	if (hipMalloc((void **)&c->d_fdir, (size_t)slots * 16) != hipSuccess ||
+	    hipMemcpy(c->d_fdir, tab, (size_t)slots * 16, hipMemcpyHostToDevice) != hipSuccess) {
+		hipFree(c->d_fdir);
+		c->d_fdir = NULL;
+		rc = -ENOMEM;
+	} else {
+		c->fdir_mask = slots - 1;
+		c->fdir_fg = IXG_ETH_MAX_TOTAL_FG + cpu_id;
+	}
+	free(tab);
+	return rc;
 }
 
 int ixg_rx_set_split(void *vctx, uint32_t split)

@@ -51,7 +51,25 @@ struct ixg_kparams {
 	uint32_t n_listen;
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
+	/* flow director (ixg_rx_set_fdir): open-addressing table of fdir_mask+1
+	 * slots of 4 u32 {src, dst, sport | dport << 16 (host order), 1 = used},
+	 * slot = ixg_fdir_hash(...) & fdir_mask, linear probing; fdir_mask 0 = off */
+	const uint32_t *fdir;
+	uint32_t fdir_mask;
+	uint32_t fdir_fg;      /* IXG_ETH_MAX_TOTAL_FG + cpu_id */
 };
+
+/* the flow-director table's hash (host and device agree on it) */
+#ifdef __HIPCC__
+#define IXG_HD __host__ __device__
+#else
+#define IXG_HD
+#endif
+IXG_HD static inline uint32_t ixg_fdir_hash(uint32_t src, uint32_t dst, uint32_t ports)
+{
+	uint32_t h = src * 0x9E3779B1u ^ dst * 0x85EBCA77u ^ ports * 0xC2B2AE3Du;
+	return h ^ (h >> 15) ^ (h >> 27);
+}
 typedef struct ixg_kparams ixg_kparams;
 
 #define IXG_ZERO_PAGE 4096u

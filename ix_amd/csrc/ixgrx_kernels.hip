@@ -467,6 +467,23 @@ DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixD
   }
   s.l4_acc = acc;
   s.stream = kind != 0 && seg_end > (uint32_t)(4 * NDW);
+  // ---- [NIC] flow-director perfect filters (ixg_rx_set_fdir): a matching
+  // IPv4 TCP frame has FLM set, so the driver gives it MBUF_INVALID_FG_ID
+  // (ixgbe.c:329-330) and eth_recv_handle_fg_transition the CPU's outbound
+  // group (ethfg.c:504-505)
+  if (SHAPE != kShapeV6 && p.fdir_mask != 0u && rss4 && proto == 6u) {
+    uint32_t k = ixg_fdir_hash(src, dst, s.ports) & p.fdir_mask;
+    for (;;) {
+      const u32x4 e = reinterpret_cast<const u32x4*>(p.fdir)[k];
+      if (e.w == 0u) break;
+      if (e.x == src && e.y == dst && e.z == s.ports) {
+        s.fg = p.fdir_fg;
+        s.flags |= IXG_RF_FDIR;
+        break;
+      }
+      k = (k + 1u) & p.fdir_mask;
+    }
+  }
 }
 
 // The record for a lane given its L4 residual: the residual computed, or a
@@ -661,7 +678,6 @@ DEV uint64_t piece_sum(const u32x4& v, int rem) {
 constexpr int kG = 16;
 constexpr int kRoundPk = 64 / kG;
 constexpr int kT = 8;
-constexpr int kQGroups = 4;  // groups of 64 chunks per wave per chunk-list fill
 
 struct WaveLds {  // per-wave scratch, LDS address space
   lds_u32* list;  // compacted long lanes

@@ -40,7 +40,7 @@ VERDICTS = {
 }
 V = {name: code for code, name in VERDICTS.items()}
 
-RF_IP_CSUM_CHECKED, RF_IP_CSUM_OK, RF_L4_CSUM_CHECKED, RF_L4_CSUM_OK, RF_RSS = 1, 2, 4, 8, 16
+RF_IP_CSUM_CHECKED, RF_IP_CSUM_OK, RF_L4_CSUM_CHECKED, RF_L4_CSUM_OK, RF_RSS, RF_FDIR = 1, 2, 4, 8, 16, 32
 
 # symbols include/ixgrx.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -48,8 +48,13 @@ EXPORTS = (
     "ixg_rx_hash_tables", "ixg_abi_version", "ixg_strerror", "ixg_rx_dispatch",
     "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg_rx_demux_batch_dev",
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
-    "ixg_ev_batch_dev", "ixg_rx_set_split",
+    "ixg_ev_batch_dev", "ixg_rx_set_split", "ixg_rx_set_fdir",
 )
+
+# struct ixg_fdir_filter (12 bytes): raw IPs as in the frame, host-order ports
+FDIR_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("src_port", "<u2"), ("dst_port", "<u2")])
+assert FDIR_DTYPE.itemsize == 12
+IXG_ETH_MAX_TOTAL_FG = 8192
 
 # enum ixg_split (ixg_rx_set_split): how a context's launches divide a batch
 SPLITS = {"auto": 0, "fast": 1, "short": 2, "long": 3, "general": 4}
@@ -126,6 +131,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_dispatch.restype = u32
     lib.ixg_rx_set_split.argtypes = [vp, u32]
     lib.ixg_rx_set_split.restype = i32
+    lib.ixg_rx_set_fdir.argtypes = [vp, vp, u32, ctypes.c_uint16]
+    lib.ixg_rx_set_fdir.restype = i32
     if lib.ixg_abi_version() != ABI_VERSION:
         raise RuntimeError("libixgrx ABI version mismatch")
     _libs[path] = lib
@@ -168,6 +175,12 @@ class RxEngine:
 
     def set_split(self, split: str) -> None:
         _check(self._lib.ixg_rx_set_split(self._ctx, SPLITS[split]), "ixg_rx_set_split", self._lib)
+
+    def set_fdir(self, filters, cpu_id: int = 0) -> None:
+        """Flow-director perfect filters (FDIR_DTYPE array; empty = none)."""
+        f = np.ascontiguousarray(filters if filters is not None else np.zeros(0, FDIR_DTYPE), dtype=FDIR_DTYPE)
+        _check(self._lib.ixg_rx_set_fdir(self._ctx, f.ctypes.data if len(f) else None, len(f), cpu_id),
+               "ixg_rx_set_fdir", self._lib)
 
     def close(self) -> None:
         if self._ctx:

@@ -299,8 +299,15 @@ static void set_drop(struct ixg_rx_rec *r, uint8_t v)
 	r->tcp_flags = 0;
 }
 
-static void rx_one(const struct ixg_rx_cfg *cfg, const struct hashtab *ht, const uint8_t *frame,
-		   uint32_t L, struct ixg_rx_rec *r, uint32_t *csum, int work)
+/* the flow-director perfect filters of ixgo_rx_batch_fdir (ixg_rx_set_fdir) */
+struct fdir_set {
+	const struct ixg_fdir_filter *f;
+	uint32_t n;
+	uint16_t cpu_id;
+};
+
+static void rx_one(const struct ixg_rx_cfg *cfg, const struct hashtab *ht, const struct fdir_set *fd,
+		   const uint8_t *frame, uint32_t L, struct ixg_rx_rec *r, uint32_t *csum, int work)
 {
 	struct frame fr = {frame, L}, *f = &fr;
 	uint32_t rss = 0;
@@ -357,6 +364,20 @@ static void rx_one(const struct ixg_rx_cfg *cfg, const struct hashtab *ht, const
 	/* fg_id = rx_fgs[rss & (nb_rx_fgs-1)].fg_id (ixgbe.c:329-335, init.c:456-462) */
 	r->fg_id = (uint16_t)(cfg->dev_idx * IXG_ETH_MAX_NUM_FG + (rss & (uint32_t)(cfg->nb_rx_fgs - 1)));
 	r->rss_hash = rss;
+	/* [NIC] a flow-director perfect filter on the 4-tuple of an IPv4 TCP
+	 * frame: FLM -> MBUF_INVALID_FG_ID (ixgbe.c:329-330) -> outbound_fg_idx()
+	 * = ETH_MAX_TOTAL_FG + cpu_id (ethfg.c:504-505, ethfg.h:135-138) */
+	if (fd && fd->n && hdr_ok && !frag && proto == 6 && l4 + 4 <= L) {
+		const uint32_t src = Braw32(f, 26), dst = Braw32(f, 30);
+		const uint16_t sp = B16(f, l4), dp = B16(f, l4 + 2);
+		for (uint32_t k = 0; k < fd->n; k++)
+			if (fd->f[k].src_ip == src && fd->f[k].dst_ip == dst && fd->f[k].src_port == sp &&
+			    fd->f[k].dst_port == dp) {
+				r->fg_id = (uint16_t)(IXG_ETH_MAX_TOTAL_FG + fd->cpu_id);
+				flags |= IXG_RF_FDIR;
+				break;
+			}
+	}
 
 	/* [NIC] L4 checksum: TCP always, UDP when the checksum field is non-zero
 	 * (RFC 768), over the IP-derived L4 length (what lwIP would pass as
@@ -526,7 +547,7 @@ void ixgo_rx_one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t le
 		}
 		ht = ht_cache;
 	}
-	rx_one(cfg, ht, frame, len, rec, csum, work);
+	rx_one(cfg, ht, NULL, frame, len, rec, csum, work);
 	if (csum && work == IXGO_WORK_FULL)
 		fix_icmp_residual(frame, len, csum);
 }
@@ -544,6 +565,7 @@ struct job {
 	struct ixg_rx_rec *out;
 	uint32_t *csum;
 	int work;
+	const struct fdir_set *fd;
 };
 
 static void *run_job(void *arg)
@@ -563,7 +585,7 @@ static void *run_job(void *arg)
 			L = j->len[i];
 		}
 		uint32_t *c = j->csum ? &j->csum[i] : NULL;
-		rx_one(j->cfg, j->ht, fr, L, &j->out[i], c, j->work);
+		rx_one(j->cfg, j->ht, j->fd, fr, L, &j->out[i], c, j->work);
 		if (c && j->work == IXGO_WORK_FULL)
 			fix_icmp_residual(fr, L, c);
 	}
@@ -606,14 +628,24 @@ int ixgo_rx_batch(const struct ixg_rx_cfg *cfg, const uint8_t *base, const uint6
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out,
 		  uint32_t *csum, int threads, int hash_mode, int work)
 {
-	struct job j = {cfg, NULL, base, off, len, NULL, stride, 0, 0, out, csum, work};
+	struct job j = {cfg, NULL, base, off, len, NULL, stride, 0, 0, out, csum, work, NULL};
+	return run_batch(&j, n, threads, hash_mode);
+}
+
+int ixgo_rx_batch_fdir(const struct ixg_rx_cfg *cfg, const uint8_t *base, const uint64_t *off,
+		       const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out,
+		       uint32_t *csum, int threads, int hash_mode, int work, const struct ixg_fdir_filter *filters,
+		       uint32_t nf, uint16_t cpu_id)
+{
+	struct fdir_set fd = {filters, nf, cpu_id};
+	struct job j = {cfg, NULL, base, off, len, NULL, stride, 0, 0, out, csum, work, &fd};
 	return run_batch(&j, n, threads, hash_mode);
 }
 
 int ixgo_rx_batch_mbufs(const struct ixg_rx_cfg *cfg, void *const *mbufs, uint32_t n,
 			struct ixg_rx_rec *out, int threads, int hash_mode, int work)
 {
-	struct job j = {cfg, NULL, NULL, NULL, NULL, mbufs, 0, 0, 0, out, NULL, work};
+	struct job j = {cfg, NULL, NULL, NULL, NULL, mbufs, 0, 0, 0, out, NULL, work, NULL};
 	return run_batch(&j, n, threads, hash_mode);
 }
 

@@ -39,6 +39,9 @@ def lib() -> ctypes.CDLL:
         vp, u32, i32, u16, u8 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, ctypes.c_uint16, ctypes.c_uint8
         L.ixgo_rx_batch.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, u32, u32, vp, vp, i32, i32, i32]
         L.ixgo_rx_batch.restype = i32
+        L.ixgo_rx_batch_fdir.argtypes = [ctypes.POINTER(_Cfg), vp, vp, vp, u32, u32, vp, vp, i32, i32, i32, vp, u32,
+                                         u16]
+        L.ixgo_rx_batch_fdir.restype = i32
         L.ixgo_rx_batch_mbufs.argtypes = [ctypes.POINTER(_Cfg), vp, u32, vp, i32, i32, i32]
         L.ixgo_rx_batch_mbufs.restype = i32
         L.ixgo_chksum_internet.argtypes = [vp, i32]
@@ -68,9 +71,15 @@ def _cfg(key: bytes, nb: int, dev: int, flags: int) -> _Cfg:
     return c
 
 
+# struct ixg_fdir_filter (include/ixgrx.h)
+FDIR_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("src_port", "<u2"), ("dst_port", "<u2")])
+
+
 def rx_batch(key: bytes, nb: int, dev: int, flags: int, blob: np.ndarray, off, lens: np.ndarray,
-             stride: int = 0, threads: int = 1, hash_mode: int = HASH_BITSERIAL, work: int = WORK_FULL):
-    """Records ([n,16] uint8) and residual words for a batch."""
+             stride: int = 0, threads: int = 1, hash_mode: int = HASH_BITSERIAL, work: int = WORK_FULL,
+             fdir=None, cpu_id: int = 0):
+    """Records ([n,16] uint8) and residual words for a batch; `fdir`: an
+    array of FDIR_DTYPE flow-director filters (ixg_rx_set_fdir) or None."""
     n = int(lens.shape[0])
     rec = np.zeros((n, 16), dtype=np.uint8)
     cs = np.zeros(n, dtype=np.uint32)
@@ -78,6 +87,12 @@ def rx_batch(key: bytes, nb: int, dev: int, flags: int, blob: np.ndarray, off, l
     lens = np.ascontiguousarray(lens, dtype=np.uint16)
     offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
     c = _cfg(key, nb, dev, flags)
+    if fdir is not None and len(fdir):
+        fd = np.ascontiguousarray(fdir, dtype=FDIR_DTYPE)
+        lib().ixgo_rx_batch_fdir(ctypes.byref(c), blob.ctypes.data, None if offa is None else offa.ctypes.data,
+                                 lens.ctypes.data, stride, n, rec.ctypes.data, cs.ctypes.data, threads, hash_mode,
+                                 work, fd.ctypes.data, len(fd), cpu_id)
+        return rec, cs
     lib().ixgo_rx_batch(ctypes.byref(c), blob.ctypes.data, None if offa is None else offa.ctypes.data,
                         lens.ctypes.data, stride, n, rec.ctypes.data, cs.ctypes.data, threads, hash_mode, work)
     return rec, cs

@@ -19,9 +19,15 @@
  *   [WHY]  drop reason codes; checked for consistency against the observed drop
  *   [V6]   the IPv6 extension (reference drops 0x86DD); Toeplitz over 36 bytes
  *          is compute_toeplitz_hash's loop generalised, parity unpinned
+ *   [FDIR] the NIC's flow-director perfect match (the 4-tuple of a
+ *          non-fragmented IPv4 TCP frame equals an installed filter); what
+ *          the stack then does with the FLM status is the reference's own
+ *          eth_recv_handle_fg_transition (ref_ethfg.c)
  *
  * Input file  (LE): "IXGRXIN1", u32 n, u32 cfg_flags, u16 nb_rx_fgs, u16 dev_idx,
- *                   u8 key[40], u16 len[n], u32 off[n], u32 blob_len, blob.
+ *                   u8 key[40], u16 len[n], u32 off[n], u32 blob_len, blob,
+ *                   optionally "FDIR", u32 nf, u16 cpu_id, u16 0,
+ *                   struct ixg_fdir_filter[nf].
  * Output file (LE): "IXGRXOUT", u32 n, struct ixg_rx_rec[n] (16 B), u32 csum[n].
  */
 #include <stdint.h>
@@ -103,6 +109,10 @@ static uint8_t drop_reason(const uint8_t *f, uint32_t L)
 	return IXG_V_DROP_IP_PROTO;
 }
 
+static const struct ixg_fdir_filter *fdir;
+static uint32_t n_fdir;
+static unsigned int fdir_cpu;
+
 static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, uint8_t *mbuf,
 		struct ixg_rx_rec *r, uint32_t *csum, uint32_t idx)
 {
@@ -141,6 +151,20 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 	}
 	r->rss_hash = rss;
 	r->fg_id = (uint16_t)(cfg->dev_idx * 512u + (rss & (uint32_t)(cfg->nb_rx_fgs - 1)));
+	/* [FDIR] a perfect-filter match sets FLM: the driver's fg_id is
+	 * MBUF_INVALID_FG_ID (ixgbe.c:329-330), then eth_recv maps it */
+	if (n_fdir && hdr_ok && !frag && proto == 6 && l4 + 4 <= L) {
+		for (uint32_t k = 0; k < n_fdir; k++)
+			if (fdir[k].src_ip == raw32(f + 26) && fdir[k].dst_ip == raw32(f + 30) &&
+			    fdir[k].src_port == B16z(f, L, l4) && fdir[k].dst_port == B16z(f, L, l4 + 2)) {
+				uint32_t fg = ref_fg_transition(0xFFFF, fdir_cpu);
+				if (fg > 0xffff)
+					die("outbound flow group not processed on its CPU", idx);
+				r->fg_id = (uint16_t)fg;
+				flags |= IXG_RF_FDIR;
+				break;
+			}
+	}
 
 	/* [NIC] L4 checksum */
 	int l4c = 0;
@@ -304,6 +328,17 @@ int main(int argc, char **argv)
 	uint8_t *blob = malloc(blob_len + 1);
 	if (fread(blob, 1, blob_len, fi) != blob_len)
 		die("short blob", 0);
+	char tag[4];
+	if (fread(tag, 1, 4, fi) == 4 && !memcmp(tag, "FDIR", 4)) {
+		uint16_t cpu, pad;
+		if (fread(&n_fdir, 4, 1, fi) != 1 || fread(&cpu, 2, 1, fi) != 1 || fread(&pad, 2, 1, fi) != 1)
+			die("short fdir header", 0);
+		struct ixg_fdir_filter *ff = malloc(sizeof(*ff) * (n_fdir + 1));
+		if (!ff || fread(ff, sizeof(*ff), n_fdir, fi) != n_fdir)
+			die("short fdir filters", 0);
+		fdir = ff;
+		fdir_cpu = cpu;
+	}
 	fclose(fi);
 
 	if (ref_ix_init())

@@ -15,6 +15,9 @@ struct ref_capture {
 extern struct ref_capture ref_cap;
 
 int ref_ix_init(void);
+/* eth_recv_handle_fg_transition (dp/core/ethfg.c:502-523) on CPU `cpu`: the
+ * fg_id it leaves, 0xffffffff when the frame would not be processed here */
+uint32_t ref_fg_transition(uint32_t fg_id, unsigned int cpu);
 void ref_eth_input(void *mbuf);
 uint16_t ref_chksum_internet(const void *buf, int len);
 

@@ -25,7 +25,8 @@ DEFINE_PERCPU(struct mempool, mbuf_mempool);
 DEFINE_PERCPU(struct eth_tx_queue *, eth_txqs[NETHDEV]);
 
 /* ---- globals (normally dp/core/ethfg.c, cfg.c, control_plane.c) ---- */
-struct eth_fg *fgs[ETH_MAX_TOTAL_FG + NCPU];
+/* weak: ixref_rx links dp/core/ethfg.c (ref_ethfg.c), which defines it */
+__attribute__((weak)) struct eth_fg *fgs[ETH_MAX_TOTAL_FG + NCPU];
 struct cfg_parameters CFG;
 int cycles_per_us = 1000;
 

@@ -31,7 +31,20 @@ F_NO_CSUM_DROP = 1
 F_IPV6 = 2
 
 
-def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int):
+def fdir_filter(f: bytes, swap: bool = False) -> bytes:
+    """struct ixg_fdir_filter matching frame f's 4-tuple (src ip, dst ip,
+    sport, dport of an IPv4 frame with ihl from byte 14); swap: the reverse
+    direction (does not match f)."""
+    l4 = 14 + 4 * (f[14] & 15)
+    src, dst = struct.unpack_from("<I", f, 26)[0], struct.unpack_from("<I", f, 30)[0]
+    sp, dp = (f[l4] << 8) | f[l4 + 1], (f[l4 + 2] << 8) | f[l4 + 3]
+    if swap:
+        src, dst, sp, dp = dst, src, dp, sp
+    return struct.pack("<IIHH", src, dst, sp, dp)
+
+
+def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir: list[bytes] | None = None,
+            cpu: int = 0):
     lens = np.array([len(f) for f in frames], dtype=np.uint16)
     offs = np.zeros(len(frames), dtype=np.uint32)
     if frames:
@@ -47,6 +60,10 @@ def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int):
             f.write(offs.tobytes())
             f.write(struct.pack("<I", len(blob)))
             f.write(blob)
+            if fdir:
+                f.write(b"FDIR")
+                f.write(struct.pack("<IHH", len(fdir), cpu, 0))
+                f.write(b"".join(fdir))
         subprocess.run([HARNESS, fi, fo], check=True)
         raw = open(fo, "rb").read()
     assert raw[:8] == b"IXGRXOUT"
@@ -281,14 +298,19 @@ def fuzz_frames(rng: np.random.Generator, n: int) -> list[bytes]:
     return out
 
 
-def save(name: str, frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, note: str):
-    rec, csum = run_ref(frames, key, nb, dev, flags)
+def save(name: str, frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, note: str,
+         fdir: list[bytes] | None = None, cpu: int = 0):
+    rec, csum = run_ref(frames, key, nb, dev, flags, fdir, cpu)
     tr = traces.pack(frames)
     path = os.path.join(HERE, name + ".npz")
+    extra = {}
+    if fdir:
+        # struct ixg_fdir_filter rows (12 bytes each) and the CPU they steer to
+        extra = {"fdir": np.frombuffer(b"".join(fdir), np.uint8).reshape(-1, 12), "fdir_cpu": np.uint16(cpu)}
     np.savez_compressed(path, blob=tr.blob, off=tr.off, len=tr.len,
                         key=np.frombuffer(key, np.uint8), nb_rx_fgs=np.uint16(nb),
                         dev_idx=np.uint16(dev), flags=np.uint32(flags), rec=rec, csum=csum,
-                        note=np.array(note))
+                        note=np.array(note), **extra)
     v = rec[:, 2]
     print(f"{name}: {len(frames)} frames, verdicts {dict(zip(*np.unique(v, return_counts=True)))}")
 
@@ -322,6 +344,27 @@ def main():
     save("randkey_fg16", tcp64[:200] + mix[:200], key2, 16, 1, 0, "random RSS key, 16 groups, dev 1")
     save("ipv6ext", v6 + edge[:80] + mix[:40], key, 128, 0, F_IPV6,
          "IXG_F_IPV6 extension (v6 RSS over 36 B is unpinned; v6 L4 checksum from ip6_chksum_pseudo_partial)")
+    # flow director: filters for a third of the TCP frames (every option
+    # length, long and short), the reverse direction of others (no match),
+    # UDP / fragment / bad-checksum frames carrying a filtered tuple
+    tcp = [f for f in tcp64 + mix if f[23] == 6]
+    hit = tcp[::3]
+    filt = [fdir_filter(f) for f in hit] + [fdir_filter(f, swap=True) for f in tcp[1::7]]
+    udp_same = []
+    for f in hit[:40]:
+        g = bytearray(f)
+        g[23] = 17  # same tuple, UDP: the TCP filter does not apply
+        udp_same.append(bytes(g))
+    frag_same = []
+    for f in hit[40:80]:
+        g = bytearray(f)
+        g[20] |= 0x20  # MF: a fragment, no L4 match
+        frag_same.append(bytes(g))
+    badc_hit = [bytes(bytearray(f[:24]) + bytes([f[24] ^ 1]) + f[25:]) for f in hit[80:120]]
+    filt += [fdir_filter(f) for f in badc_hit]
+    save("fdir", tcp + udp_same + frag_same + badc_hit + edge[:120] + fuzz[:300], key, 64, 2, 0,
+         "flow-director filters (FLM -> outbound flow group 8192 + cpu 5), nb_rx_fgs 64, dev_idx 2",
+         fdir=filt, cpu=5)
 
 
 if __name__ == "__main__":

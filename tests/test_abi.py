@@ -108,3 +108,14 @@ def test_tx_seg_layout_matches_header():
         got = [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
     assert got[0] == tx.SEG_DTYPE.itemsize
     assert got[1:] == [tx.SEG_DTYPE.fields[f][1] for f in fields]
+
+
+def test_null_context_entry_points():
+    """Every context entry point rejects a NULL context with -EINVAL before
+    touching the device (CPU-checkable part of the ABI)."""
+    lib = ixgrx.load_library()
+    assert lib.ixg_rx_set_split(None, 0) == -22
+    assert lib.ixg_rx_set_fdir(None, None, 0, 0) == -22
+    assert lib.ixg_rx_batch_mbufs(None, None, 0, None) == -22
+    assert lib.ixg_rx_batch_host(None, None, None, None, 0, 0, None, None) == -22
+    assert ixgrx.FDIR_DTYPE.itemsize == 12

@@ -54,7 +54,12 @@ def engines(request):
 
 def test_golden_fixtures(golden, engines):
     eng = engines(bytes(golden["key"]), int(golden["nb_rx_fgs"]), int(golden["dev_idx"]), int(golden["flags"]))
-    rec, cs = eng.batch_host(golden["blob"], golden["off"], golden["len"], want_csum=True)
+    if "fdir" in golden:  # the flow-director fixture: the reference's outbound-group mapping
+        eng.set_fdir(np.ascontiguousarray(golden["fdir"]).view(ixgrx.FDIR_DTYPE).reshape(-1), int(golden["fdir_cpu"]))
+    try:
+        rec, cs = eng.batch_host(golden["blob"], golden["off"], golden["len"], want_csum=True)
+    finally:
+        eng.set_fdir(None)
     _diff(rec, golden["rec"], golden["name"])
     bad = np.nonzero(cs != golden["csum"])[0]
     assert bad.size == 0, f"residuals differ at {bad[:8].tolist()}"
@@ -466,4 +471,48 @@ def test_mbufs_reject_oversized_len():
         eng.batch_mbufs(ptrs)  # the maximum itself is accepted
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("kind,layout", [("tcp64", "stride"), ("tcp64", "packed"), ("imix", "packed"),
+                                         ("mixed", "packed"), ("tcp1514", "stride")])
+def test_fdir_vs_oracle(kind, layout, engines):
+    """Flow-director filters over every kernel and layout: filters for a
+    quarter of the batch's TCP flows (plus reverse-direction ones that must
+    not match), checked against the oracle; then the filters are removed and
+    the records are the plain RSS ones again."""
+    import torch
+    n = 20000
+    tr = traces.make_trace(kind, n, seed=0x1B7200 + n, bad_ip=0.01, bad_l4=0.01)
+    if layout == "packed" and tr.off is None:
+        tr = traces.Trace(tr.blob, tr.offsets().copy(), tr.len, 0)
+    offs = tr.offsets().astype(np.int64)
+    b = tr.blob
+    tcp = np.nonzero((b[offs + 12] == 8) & (b[offs + 13] == 0) & (b[offs + 23] == 6))[0]
+    pick = tcp[::4]
+    l4 = offs[pick] + 14 + 4 * (b[offs[pick] + 14] & 15).astype(np.int64)
+    f = np.zeros(len(pick) * 2, ixgrx.FDIR_DTYPE)
+    for k, (src, dst, sp, dp) in enumerate(((26, 30, 0, 2), (30, 26, 2, 0))):
+        rows = f[k::2]
+        rows["src_ip"] = b[(offs[pick] + src)[:, None] + np.arange(4)].view("<u4").reshape(-1)
+        rows["dst_ip"] = b[(offs[pick] + dst)[:, None] + np.arange(4)].view("<u4").reshape(-1)
+        rows["src_port"] = (b[l4 + sp].astype(np.uint16) << 8) | b[l4 + sp + 1]
+        rows["dst_port"] = (b[l4 + dp].astype(np.uint16) << 8) | b[l4 + dp + 1]
+    eng = engines()
+    er, _ = oracle.rx_trace(tr, KEY, threads=8, fdir=f, cpu_id=9)
+    assert ((er[:, 3] & 0x20) != 0).sum() >= len(pick) // 2
+    eng.set_fdir(f, cpu_id=9)
+    try:
+        dev = torch.device("cuda:0")
+        blob = torch.from_numpy(np.concatenate([tr.blob, np.zeros(64, np.uint8)])).to(dev)
+        lens = torch.from_numpy(tr.len.view(np.int16)).to(dev)
+        off = None if tr.off is None else torch.from_numpy(tr.off.view(np.int64)).to(dev)
+        out = torch.zeros((n, 16), dtype=torch.uint8, device=dev)
+        eng.batch_dev(blob.data_ptr(), None if off is None else off.data_ptr(), lens.data_ptr(), tr.stride, n,
+                      out.data_ptr(), None, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        _diff(out.cpu().numpy(), er, f"fdir {kind} {layout}")
+    finally:
+        eng.set_fdir(None)
+    plain, _ = oracle.rx_trace(tr, KEY, threads=8)
+    _diff(eng.batch_trace(tr), plain, f"fdir removed {kind} {layout}")
 

@@ -13,11 +13,19 @@ from oracle import oracle
 from ix_amd import traces
 
 
+def _fdir(golden):
+    """The fixture's flow-director filters (FDIR_DTYPE) and CPU, or (None, 0)."""
+    if "fdir" not in golden:
+        return None, 0
+    return np.ascontiguousarray(golden["fdir"]).view(oracle.FDIR_DTYPE).reshape(-1), int(golden["fdir_cpu"])
+
+
 @pytest.mark.parametrize("hash_mode", [oracle.HASH_BITSERIAL, oracle.HASH_TABLE])
 def test_oracle_matches_reference(golden, hash_mode):
+    fd, cpu = _fdir(golden)
     rec, cs = oracle.rx_batch(bytes(golden["key"]), int(golden["nb_rx_fgs"]), int(golden["dev_idx"]),
                               int(golden["flags"]), golden["blob"], golden["off"], golden["len"],
-                              hash_mode=hash_mode)
+                              hash_mode=hash_mode, fdir=fd, cpu_id=cpu)
     exp = golden["rec"]
     bad = np.nonzero((rec != exp).any(axis=1))[0]
     assert bad.size == 0, f"{golden['name']}: {bad.size} records differ, first {bad[:8]}: " \
@@ -27,10 +35,13 @@ def test_oracle_matches_reference(golden, hash_mode):
 
 
 def test_oracle_threads_match_single(golden):
+    fd, cpu = _fdir(golden)
     a = oracle.rx_batch(bytes(golden["key"]), int(golden["nb_rx_fgs"]), int(golden["dev_idx"]),
-                        int(golden["flags"]), golden["blob"], golden["off"], golden["len"], threads=1)
+                        int(golden["flags"]), golden["blob"], golden["off"], golden["len"], threads=1, fdir=fd,
+                        cpu_id=cpu)
     b = oracle.rx_batch(bytes(golden["key"]), int(golden["nb_rx_fgs"]), int(golden["dev_idx"]),
-                        int(golden["flags"]), golden["blob"], golden["off"], golden["len"], threads=4)
+                        int(golden["flags"]), golden["blob"], golden["off"], golden["len"], threads=4, fdir=fd,
+                        cpu_id=cpu)
     assert (a[0] == b[0]).all() and (a[1] == b[1]).all()
 
 
@@ -96,3 +107,19 @@ def test_chksum_internet_rfc1071_example():
     assert res == (~0xF2DD) & 0xFFFF
     z = np.zeros(20, np.uint8)
     assert L.ixgo_chksum_internet(z.ctypes.data, 20) == 0xFFFF  # all-zero header is invalid
+
+
+def test_fdir_fixture_pins_the_outbound_group():
+    """The flow-director fixture's matches carry the reference's outbound
+    flow group (eth_recv_handle_fg_transition: ETH_MAX_TOTAL_FG + cpu_id) and
+    IXG_RF_FDIR; frames of the same tuple that are UDP or fragments do not
+    match."""
+    from conftest import load_golden
+    g = load_golden("fdir")
+    rec = g["rec"]
+    fg = rec[:, 0].astype(np.int64) | (rec[:, 1].astype(np.int64) << 8)
+    hit = (rec[:, 3] & 0x20) != 0
+    assert hit.sum() >= 250
+    assert (fg[hit] == 8192 + int(g["fdir_cpu"])).all()
+    assert (fg[~hit] < 8192).all()
+
