@@ -623,6 +623,97 @@ def xgmi_leg(wl, eng, dist, world: int, rank: int, reps: int = 3):
                     "records to GPU 0", "parity": "tiled-consistent" if ok else "MISMATCH"}
 
 
+C4_FRAMES = 64 * 1024 * 1024  # BASELINE.json configs[3]: one 64M-frame batch of 1514-B frames
+
+
+def strong_leg(dev, run_slice, dist, world: int, rank: int, n_total: int = C4_FRAMES, pool: int = 1 << 13,
+               reps: int = 3):
+    """C4 as BASELINE.json states it (configs[3], SURVEY.md 8(e) option 1):
+    ONE batch of n_total 1514-B frames (stride 1516) that starts in GPU 0's
+    HBM, split by shard.shard_bounds into contiguous slices; grouped RCCL
+    send/recv hand every rank its slice over xGMI, every rank runs the
+    kernels on its slice, and the 16-byte records come back into the
+    batch's record array on GPU 0. Strong scaling: the batch is the same at
+    every N (at N=1 there is nothing to move). Scatter, kernel and gather
+    are timed separately, each bracketed by synchronize + barrier, max over
+    ranks; the best of `reps` rounds. `run_slice(blob, lens, stride, m, out,
+    stream)` runs the hot path on one slice (the HIP engine in bench.py;
+    the oracle in the gloo test of this leg, tests/test_multi.py)."""
+    import torch
+    from ix_amd import shard, traces
+    cuda = dev.type == "cuda"
+
+    def sync():
+        if cuda:
+            torch.cuda.synchronize()
+
+    def barrier():
+        sync()
+        if world > 1:
+            dist.barrier()
+        sync()
+
+    # every rank derives the batch's lengths from the same pool; only rank
+    # 0 materialises the batch
+    pool_tr = traces.make_trace("tcp1514", pool, seed=0x1B4C4)
+    S = pool_tr.stride
+    bounds = shard.shard_bounds(np.tile(pool_tr.len, n_total // pool), world)
+    s, e = bounds[rank]
+    wl = Workload("c4", seed=0x1B4C4, dev=dev, n=n_total, pool=pool) if rank == 0 else None
+    stream = torch.cuda.current_stream().cuda_stream if cuda else None
+    out = wl.out if rank == 0 else torch.empty((e - s, 16), dtype=torch.uint8, device=dev)
+    mine = out[s:e] if rank == 0 else out
+    best = None
+    for _ in range(reps):
+        ts = []
+        barrier()
+        t0 = time.perf_counter()
+        if world > 1:
+            blob, lens = shard.scatter_frames(wl.blob if wl else None, wl.len if wl else None, S, bounds, dist, dev)
+        else:
+            blob, lens = wl.blob, wl.len
+        barrier()
+        ts.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        if e > s:
+            run_slice(blob, lens, S, e - s, mine, stream)
+        barrier()
+        ts.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        if world > 1:
+            shard.gather_frame_records(mine, bounds, dist, out if rank == 0 else None)
+        barrier()
+        ts.append(time.perf_counter() - t0)
+        if world > 1:
+            ts = [shard.max_over_ranks(t, dist, device="cuda" if dist.get_backend() == "nccl" else "cpu")
+                  for t in ts]
+        best = ts if best is None or sum(ts) < sum(best) else best
+        del blob, lens
+    sc, kr, ga = best
+    sizes = [b - a for a, b in bounds]
+    res = {"workload": f"C4 (configs[3]): one batch of {n_total} x 1514B IPv4/TCP frames (stride {S}) in GPU 0's "
+                       f"HBM, split by shard_bounds across {world} GPU(s)",
+           "scaling": "strong", "frames": n_total, "slice_frames": [min(sizes), max(sizes)],
+           "scatter_ms": round(sc * 1e3, 3), "kernel_ms": round(kr * 1e3, 3), "gather_ms": round(ga * 1e3, 3),
+           "mpps_device_resident": round(n_total / kr / 1e6, 2),
+           "mpps_end_to_end": round(n_total / (sc + kr + ga) / 1e6, 2),
+           "note": "kernel = every rank's slice already in its own HBM (slowest rank); end_to_end adds the xGMI "
+                   "scatter of frames from GPU 0 (grouped RCCL send/recv, one per peer) and the gather of records"}
+    if world > 1:
+        res["scatter_gbps"] = round((n_total - sizes[0]) * S / sc / 1e9, 1)
+        res["gather_gbps"] = round((n_total - sizes[0]) * 16 / ga / 1e9, 1)
+    alg = float(alg_bytes(pool_tr).mean())
+    res["alg_bytes_per_pkt"] = round(alg, 1)
+    res["roofline_frac_per_gpu"] = round(alg * max(sizes) / kr / 1e9 / PEAK_HBM_GBPS, 4)
+    check = None
+    if rank == 0:
+        tiled, first = wl.snapshot()
+        check = ("rx", "c4_strong", wl.pool, wl.flags, first, tiled)
+        res["parity"] = "tiled-consistent" if tiled else "MISMATCH"
+        del wl
+    return res, check
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -648,7 +739,9 @@ def main():
     ap.add_argument("--no-demux", action="store_true")
     ap.add_argument("--no-tx", action="store_true")
     ap.add_argument("--no-bad", action="store_true", help="skip the C2 bad-checksum line")
-    ap.add_argument("--xgmi", action="store_true", help="N > 1: add the scatter/gather-over-xGMI leg")
+    ap.add_argument("--xgmi", action="store_true", help="N > 1: add the equal-slice RCCL scatter/gather leg")
+    ap.add_argument("--no-strong", action="store_true", help="skip the C4 one-batch strong-split line")
+    ap.add_argument("--strong-n", type=int, default=C4_FRAMES, help="C4 strong-split batch size (frames)")
     ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
     args = ap.parse_args()
 
@@ -751,6 +844,17 @@ def main():
                             "alg_bytes_per_pkt": round(wl2.bytes_per_pkt, 1),
                             "parity": "tiled-consistent" if tiled2 else "MISMATCH"}
         wl = wl2
+    if not args.no_strong and args.workload == "c2":
+        del wl
+        wl = None
+        torch.cuda.empty_cache()
+
+        def run_slice(blob, lens, S, m, out, stream):
+            engine(0).batch_dev(blob.data_ptr(), None, lens.data_ptr(), S, m, out.data_ptr(), None, stream)
+        res["c4_strong"], schk = strong_leg(dev, run_slice, dist, world, rank, n_total=args.strong_n)
+        if schk:
+            checks.append(schk)
+        torch.cuda.empty_cache()
     if not args.no_demux and args.workload == "c2":
         del wl
         torch.cuda.empty_cache()
@@ -791,6 +895,8 @@ def main():
         res["parity"] = par[wl_name]
         if "secondary" in res:
             res["secondary"]["parity"] = par[args.secondary]
+        if "c4_strong" in res:
+            res["c4_strong"]["parity"] = par["c4_strong"]
         if "demux" in res:
             res["demux"]["parity"] = par["demux"]
             res["demux"]["kinds"] = par["demux_kinds"]

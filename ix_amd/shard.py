@@ -10,8 +10,11 @@ xGMI on the data path. Records come back in input order through
 ``gather_records``: an all-gather of fixed-size 16-byte records.
 
 When the batch instead starts in one GPU's HBM (SURVEY.md 8(e) option 1),
-``scatter_slices`` / ``gather_slices`` move equal-sized slices out and the
-records back over xGMI with one RCCL scatter and one gather.
+``scatter_frames`` / ``gather_frame_records`` move each rank's
+``shard_bounds`` slice out and its records back over xGMI as grouped RCCL
+send/recv (one pair per peer; slices may differ in size), and
+``scatter_slices`` / ``gather_slices`` do the same for equal-sized slices
+with one RCCL scatter and one gather. bench.py's C4 line is the first.
 """
 from __future__ import annotations
 
@@ -98,6 +101,95 @@ def gather_slices(part, dist, dst: int = 0):
         return full.view((world * part.shape[0],) + tuple(part.shape[1:]))
     dist.gather(part, dst=dst)
     return None
+
+
+def _p2p(ops, dist) -> None:
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+def _host_staged(dist, t) -> bool:
+    """gloo moves host tensors only: device tensors are staged through host
+    memory (the CPU rehearsal of the split; RCCL sends HBM to HBM)."""
+    return t is not None and t.is_cuda and dist.get_backend() != "nccl"
+
+
+def scatter_frames(blob, lens, stride: int, bounds, dist, device, src: int = 0):
+    """C4's split (SURVEY.md 8(e) option 1) for a fixed-stride batch: rank
+    `src` holds the whole batch (`blob`: n * stride frame bytes + TAIL_PAD,
+    `lens`: n int16 lengths; None on the other ranks) and every other rank r
+    receives frames [s_r, e_r) of `bounds` (shard_bounds: unequal slices are
+    fine). One grouped send/recv per peer (RCCL batches them into one group,
+    so the slices leave GPU `src` over their own xGMI links at once).
+
+    Returns this rank's (blob, lens) on `device`, ready for ixg_rx_batch_dev:
+    on `src` they are views into the batch (the frames after the slice, or
+    the batch's own tail pad, cover the TAIL_PAD the device API reads past
+    the last frame); elsewhere fresh buffers with a zeroed tail pad. All
+    ranks must call it; bracket it with a barrier when timing it."""
+    import torch
+    rank = dist.get_rank()
+    s, e = bounds[rank]
+    m = e - s
+    P = dist.P2POp
+    if rank == src:
+        if blob.numel() < len(lens) * stride + TAIL_PAD or bounds[-1][1] != len(lens):
+            raise ValueError("blob/lens do not hold the whole batch the bounds describe")
+        ops = []
+        for r, (a, b) in enumerate(bounds):
+            if r == src or b <= a:
+                continue
+            fb, lb = blob[a * stride:b * stride], lens[a:b]
+            if _host_staged(dist, fb):
+                fb, lb = fb.cpu(), lb.cpu()
+            ops += [P(dist.isend, fb, r), P(dist.isend, lb, r)]
+        _p2p(ops, dist)
+        return blob[s * stride:], lens[s:e]
+    out_blob = torch.zeros(m * stride + TAIL_PAD, dtype=torch.uint8, device=device)
+    out_lens = torch.empty(m, dtype=torch.int16, device=device)
+    if m:
+        rb, rl = out_blob[:m * stride], out_lens
+        staged = _host_staged(dist, rb)
+        if staged:
+            rb, rl = torch.empty(m * stride, dtype=torch.uint8), torch.empty(m, dtype=torch.int16)
+        _p2p([P(dist.irecv, rb, src), P(dist.irecv, rl, src)], dist)
+        if staged:
+            out_blob[:m * stride].copy_(rb)
+            out_lens.copy_(rl)
+    return out_blob, out_lens
+
+
+def gather_frame_records(rec, bounds, dist, out=None, dst: int = 0):
+    """The reverse of scatter_frames: every rank's [e_r - s_r, 16] records
+    land in rows [s_r, e_r) of `out` ([n, 16] uint8 on rank `dst`; None
+    elsewhere), one grouped send/recv per peer. On `dst`, `rec` may already
+    be the view out[s:e] (the kernels wrote there): then nothing is copied.
+    Returns `out` on dst, None elsewhere."""
+    import torch
+    rank = dist.get_rank()
+    P = dist.P2POp
+    if rank != dst:
+        if rec.shape[0]:
+            t = rec.cpu() if _host_staged(dist, rec) else rec
+            _p2p([P(dist.isend, t, dst)], dist)
+        return None
+    s, e = bounds[rank]
+    if e > s and rec.data_ptr() != out[s:e].data_ptr():
+        out[s:e].copy_(rec)
+    ops, staged = [], []
+    for r, (a, b) in enumerate(bounds):
+        if r == dst or b <= a:
+            continue
+        t = out[a:b]
+        if _host_staged(dist, t):
+            t = torch.empty((b - a, 16), dtype=torch.uint8)
+            staged.append((a, b, t))
+        ops.append(P(dist.irecv, t, r))
+    _p2p(ops, dist)
+    for a, b, t in staged:
+        out[a:b].copy_(t)
+    return out
 
 
 def max_over_ranks(x: float, dist, device="cpu") -> float:

@@ -53,6 +53,21 @@ def test_two_ranks_gloo_hip(kind, n):
     _run(2, kind, n, "hip")
 
 
+@pytest.mark.parametrize("world,n", [(2, 512 * 6), (3, 512 * 4)])
+def test_strong_split_gloo(world, n):
+    """bench.py's C4 line (one batch on rank 0, split by shard_bounds,
+    scattered, processed, records gathered) end to end over gloo; world 3
+    gives unequal slices."""
+    _run(world, "strong", n, "oracle")
+
+
+@pytest.mark.gpu
+def test_strong_split_gloo_hip():
+    """The same leg with the HIP engine on the box's one GPU (two ranks
+    sharing the card, device tensors staged through host memory by gloo)."""
+    _run(2, "strong", 512 * 64, "hip")
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_shard_bounds_balanced(world):
     tr = traces.make_trace("imix", 5000, seed=3)
