@@ -16,7 +16,8 @@
  *   [NIC]  the driver's checksum/RSS applicability rules (DESIGN.md "NIC rules")
  *   [UDP]  udp.c:59's length check (udp.c is unbuildable: needs Dune's mmu-x86.h)
  *   [TCP]  the tcp_input head glue around pbuf_header (tcp_in.c:189,221-222,240)
- *   [WHY]  drop reason codes; checked for consistency against the observed drop
+ *   [WHY]  drop reason codes, each confirmed by the reference: the blamed field
+ *          is repaired and eth_input run again (confirm_drop)
  *   [V6]   the IPv6 extension (reference drops 0x86DD); Toeplitz over 36 bytes
  *          is compute_toeplitz_hash's loop generalised, parity unpinned
  *   [FDIR] the NIC's flow-director perfect match (the 4-tuple of a
@@ -28,7 +29,9 @@
  *                   u8 key[40], u16 len[n], u32 off[n], u32 blob_len, blob,
  *                   optionally "FDIR", u32 nf, u16 cpu_id, u16 0,
  *                   struct ixg_fdir_filter[nf].
- * Output file (LE): "IXGRXOUT", u32 n, struct ixg_rx_rec[n] (16 B), u32 csum[n].
+ * Output file (LE): "IXGRXOUT", u32 n, struct ixg_rx_rec[n] (16 B), u32 csum[n],
+ *                   u8 confirm[n] (0: eth_input did not drop the frame; 1: it
+ *                   did and confirm_drop pinned the reason; 2: not pinned).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -109,12 +112,93 @@ static uint8_t drop_reason(const uint8_t *f, uint32_t L)
 	return IXG_V_DROP_IP_PROTO;
 }
 
+static void put16(uint8_t *p, uint32_t v)
+{
+	p[0] = (uint8_t)(v >> 8);
+	p[1] = (uint8_t)v;
+}
+
+/* the ICMP message's checksum rewritten so chksum_internet over it is 0 */
+static void icmp_fix(uint8_t *g, uint32_t l4, uint32_t n)
+{
+	g[l4 + 2] = g[l4 + 3] = 0;
+	uint16_t c = ref_chksum_internet(g + l4, (int)n);
+	memcpy(g + l4 + 2, &c, 2);
+}
+
+/* [WHY] pin: mend the one field (or length) drop reason `why` blames.
+ * Returns 0 when the reason has no repair. */
+static int repair(uint8_t *g, uint32_t *L, uint8_t why)
+{
+	const uint32_t ihl = g[14] & 15, l4 = 14 + ihl * 4;
+	uint32_t ip_len = ((uint32_t)g[16] << 8) | g[17];
+	switch (why) {
+	case IXG_V_DROP_ETHERTYPE: /* (a frame shorter than its Ethernet header grows) */
+		put16(g + 12, 0x0800);
+		if (*L < 14)
+			*L = 14;
+		return 1;
+	case IXG_V_DROP_IP_SHORT: *L = 34; return 1; /* the frame grows (zero bytes) */
+	case IXG_V_DROP_IP_VERSION: g[14] = (uint8_t)(0x40 | ihl); return 1;
+	case IXG_V_DROP_IP_IHL: g[14] = (uint8_t)((g[14] & 0xF0) | 5); return 1;
+	case IXG_V_DROP_IP_FRAG: g[20] &= 0x40; g[21] = 0; return 1; /* DF kept */
+	case IXG_V_DROP_IP_LEN: put16(g + 16, ihl * 4); return 1;
+	case IXG_V_DROP_IP_TRUNC:
+		if (14 + ip_len <= IXG_MBUF_DATA_LEN)
+			*L = 14 + ip_len;
+		else
+			put16(g + 16, *L - 14 >= ihl * 4 ? *L - 14 : ihl * 4);
+		if (*L < l4)
+			*L = l4;
+		return 1;
+	case IXG_V_DROP_IP_PROTO: g[23] = 17; return 1;
+	case IXG_V_DROP_ICMP_SHORT:
+		put16(g + 16, ihl * 4 + 8);
+		if (*L < l4 + 8)
+			*L = l4 + 8;
+		icmp_fix(g, l4, 8);
+		return 1;
+	case IXG_V_DROP_ICMP_CSUM: icmp_fix(g, l4, ip_len - ihl * 4); return 1;
+	case IXG_V_DROP_ICMP_TYPE: g[l4] = 8; icmp_fix(g, l4, ip_len - ihl * 4); return 1;
+	}
+	return 0;
+}
+
+/* [WHY] pin: a restated drop reason is confirmed by the reference itself.
+ * The blamed field is repaired and the reference eth_input runs again; the
+ * frame must then be delivered, or dropped for a strictly later reason (the
+ * order of the checks in eth_input/ip_input/icmp_input, ip.c:63-114,
+ * icmp.c:78-115), whose field is repaired in turn, until the reference
+ * delivers it. Returns the number of repairs, 0 when not confirmed. */
+static int confirm_drop(const uint8_t *frame, uint32_t L, uint8_t why, uint8_t *mbuf)
+{
+	uint8_t g[IXG_MBUF_DATA_LEN + 64];
+	memset(g, 0, sizeof(g));
+	memcpy(g, frame, L);
+	for (int step = 1; step <= 16; step++) {
+		if (!repair(g, &L, why) || L > IXG_MBUF_DATA_LEN)
+			return 0;
+		size_t len = L;
+		memset(mbuf, 0, IXG_MBUF_STRIDE);
+		memcpy(mbuf, &len, sizeof(len));
+		memcpy(mbuf + IXG_MBUF_HEADER_LEN, g, L);
+		ref_eth_input(mbuf);
+		if (ref_cap.kind != REF_NONE)
+			return step;
+		const uint8_t next = drop_reason(g, L);
+		if (next <= why)
+			return 0;
+		why = next;
+	}
+	return 0;
+}
+
 static const struct ixg_fdir_filter *fdir;
 static uint32_t n_fdir;
 static unsigned int fdir_cpu;
 
 static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, uint8_t *mbuf,
-		struct ixg_rx_rec *r, uint32_t *csum, uint32_t idx)
+		struct ixg_rx_rec *r, uint32_t *csum, uint8_t *confirm, uint32_t idx)
 {
 	uint8_t f[2048 + 64];
 	uint16_t ip_res = 0xffff, l4_res = 0xffff;
@@ -122,6 +206,7 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 	uint8_t flags = 0;
 
 	memset(r, 0, sizeof(*r));
+	*confirm = 0;
 	r->pcb_bucket = IXG_NO_BUCKET;
 	memset(f, 0, sizeof(f));
 	memcpy(f, frame, L); /* a pristine copy: icmp_reflect rewrites the mbuf */
@@ -242,6 +327,7 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 			die("eth_input neither delivered nor freed", idx);
 		uint8_t why = drop_reason(f, L);
 		drop(r, why);
+		*confirm = (uint8_t)(confirm_drop(f, L, why, mbuf) ? 1 : 2);
 		return;
 	}
 	case REF_TCP: {
@@ -346,10 +432,11 @@ int main(int argc, char **argv)
 	uint8_t *mbuf = aligned_alloc(64, IXG_MBUF_STRIDE);
 	struct ixg_rx_rec *recs = calloc(n + 1, sizeof(*recs));
 	uint32_t *cs = calloc(n + 1, sizeof(*cs));
+	uint8_t *cf = calloc(n + 1, 1);
 	for (uint32_t i = 0; i < n; i++) {
 		if (len[i] > IXG_MBUF_DATA_LEN || (uint64_t)off[i] + len[i] > blob_len)
 			die("frame does not fit an mbuf", i);
-		one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], i);
+		one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], &cf[i], i);
 	}
 	FILE *fo = fopen(argv[2], "wb");
 	if (!fo)
@@ -358,6 +445,7 @@ int main(int argc, char **argv)
 	fwrite(&n, 4, 1, fo);
 	fwrite(recs, sizeof(*recs), n, fo);
 	fwrite(cs, 4, n, fo);
+	fwrite(cf, 1, n, fo);
 	fclose(fo);
 	if (tsec > 0 && n > 0) {
 		struct timespec t0, t1;
@@ -366,7 +454,7 @@ int main(int argc, char **argv)
 		clock_gettime(CLOCK_MONOTONIC, &t0);
 		do {
 			for (uint32_t i = 0; i < n; i++)
-				one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], i);
+				one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], &cf[i], i);
 			done += n;
 			clock_gettime(CLOCK_MONOTONIC, &t1);
 			el = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);

@@ -71,6 +71,15 @@ def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir
     assert n == len(frames)
     rec = np.frombuffer(raw, dtype=np.uint8, count=16 * n, offset=12).reshape(n, 16).copy()
     csum = np.frombuffer(raw, dtype=np.uint32, count=n, offset=12 + 16 * n).copy()
+    confirm = np.frombuffer(raw, dtype=np.uint8, count=n, offset=12 + 20 * n)
+    # every drop eth_input made has a reference-confirmed reason: with the
+    # field the reason blames repaired, the reference eth_input delivers the
+    # frame or drops it for a strictly later reason, repaired in turn until
+    # it delivers (harness_main.c confirm_drop)
+    verdict = rec[:, 2]
+    eth_input_reasons = ((verdict >= 0x80) & (verdict <= 0x87)) | ((verdict >= 0x8b) & (verdict <= 0x8d))
+    assert not (confirm == 2).any(), f"drop reasons not confirmed by the reference: {np.nonzero(confirm == 2)[0][:20]}"
+    assert ((confirm == 1) == eth_input_reasons).all(), "a drop reason without a reference confirmation"
     return rec, csum
 
 
