@@ -23,8 +23,11 @@
 struct ixg_dstate {
 	uint8_t *d_defer;    /* one flag per 64-packet chunk */
 	size_t defer_cap;
-	uint32_t *d_present; /* [4] (ixg_kparams.present) */
+	uint32_t *d_present; /* [IXG_PRESENT_WORDS] (ixg_kparams.present) */
 	uint32_t epoch;      /* last launch's stamp */
+	uint32_t *d_tail;    /* the parse / tail split: 32 B per frame (ixg_kparams.tail) */
+	uint64_t *d_tmeta;   /* 8 B per chunk (ixg_kparams.tmeta) */
+	size_t tail_cap;     /* frames d_tail holds */
 };
 
 /* one stage of the pipelined host path (ixg_rx_batch_mbufs): pinned
@@ -202,6 +205,8 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_tab32);
 	hipFree(c->d_tab16);
 	hipFree(c->ds.d_defer);
+	hipFree(c->ds.d_tail);
+	hipFree(c->ds.d_tmeta);
 	hipFree(c->d_zero);
 	hipFree(c->ds.d_present);
 	for (int k = 0; k < IXG_SLOTS; k++) {
@@ -209,6 +214,8 @@ void ixg_rx_fini(void *vctx)
 		if (sl->stream)
 			hipStreamSynchronize(sl->stream);
 		hipFree(sl->ds.d_defer);
+		hipFree(sl->ds.d_tail);
+		hipFree(sl->ds.d_tmeta);
 		hipFree(sl->ds.d_present);
 		hipHostFree(sl->h_frames);
 		hipHostFree(sl->h_off);
@@ -324,8 +331,8 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 	}
 	if (hipMalloc((void **)&c->d_zero, IXG_ZERO_PAGE) != hipSuccess ||
 	    hipMemset(c->d_zero, 0, IXG_ZERO_PAGE) != hipSuccess ||
-	    hipMalloc((void **)&c->ds.d_present, 4 * sizeof(uint32_t)) != hipSuccess ||
-	    hipMemset(c->ds.d_present, 0, 4 * sizeof(uint32_t)) != hipSuccess)
+	    hipMalloc((void **)&c->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)) != hipSuccess ||
+	    hipMemset(c->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)) != hipSuccess)
 		goto fail;
 	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
@@ -385,6 +392,22 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 			HIPCHK(hipMalloc((void **)&ds->d_defer, cap));
 			ds->defer_cap = cap;
 		}
+#ifdef IXGRX_AB
+		/* the parse / tail split's buffers (A/B builds only) */
+		if (n > ds->tail_cap) {
+			hipFree(ds->d_tail);
+			hipFree(ds->d_tmeta);
+			ds->d_tail = NULL;
+			ds->d_tmeta = NULL;
+			ds->tail_cap = 0;
+			size_t cap = ((size_t)n + n / 4 + 4096) & ~(size_t)63;
+			HIPCHK(hipMalloc((void **)&ds->d_tail, cap * 32));
+			HIPCHK(hipMalloc((void **)&ds->d_tmeta, cap / 64 * 8));
+			ds->tail_cap = cap;
+		}
+		p.tail = ds->d_tail;
+		p.tmeta = ds->d_tmeta;
+#endif
 		p.defer = ds->d_defer;
 		p.present = ds->d_present;
 		if (++ds->epoch == 0)
@@ -568,8 +591,8 @@ static int slot_init(struct ixg_ctx *c, struct ixg_slot *sl)
 	if (!sl->done)
 		HIPCHK(hipEventCreateWithFlags(&sl->done, hipEventDisableTiming));
 	if (!sl->ds.d_present) {
-		HIPCHK(hipMalloc((void **)&sl->ds.d_present, 4 * sizeof(uint32_t)));
-		HIPCHK(hipMemset(sl->ds.d_present, 0, 4 * sizeof(uint32_t)));
+		HIPCHK(hipMalloc((void **)&sl->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)));
+		HIPCHK(hipMemset(sl->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 	}
 	const size_t fcap = IXG_PIPE_BYTES + IXG_TAIL_PAD, ncap = IXG_PIPE_FRAMES;
 	if (!sl->h_frames)

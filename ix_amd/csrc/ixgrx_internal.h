@@ -32,10 +32,22 @@ struct ixg_kparams {
 	                          kernel, IXG_CLS_SHORT / IXG_CLS_LONG = left for
 	                          that general kernel; NULL = the long general
 	                          kernel does everything */
-	uint32_t *present;     /* [4]: present[k] == epoch (k = 1, 2) iff some chunk
-	                          of class k was deferred in this launch;
-	                          present[0] == epoch iff the sampler ran, and
-	                          then present[3] is the launch's IXG_MODE_* */
+	uint32_t *present;     /* [IXG_PRESENT_WORDS]: present[k] == epoch (k = 1, 2)
+	                          iff some chunk of class k was deferred in this
+	                          launch; present[0] == epoch iff the sampler ran,
+	                          and then present[3] is the launch's IXG_MODE_*;
+	                          present[4] == epoch iff the parse kernel left
+	                          tails for the tail kernel */
+	/* the parse / tail split of the long class (with defer): the parse
+	 * kernel leaves each long L4 segment's whole 16-byte pieces past the
+	 * prefix to the tail kernel. tail: 2 x u32x4 per frame index {frame
+	 * offset lo, hi, seg_end | ip_res << 16, partial sum}, {the record if
+	 * the L4 check fails}; tmeta: per chunk the mask of its lanes with a
+	 * tail, written for every chunk the parse kernel takes (the tail kernel
+	 * takes the same chunks: no stale mask is ever read, graph replays
+	 * included) */
+	uint32_t *tail;
+	uint64_t *tmeta;
 	uint32_t epoch;        /* per-launch stamp (never 0) */
 	uint32_t force_mode;   /* IXG_MODE_* for the sampler to write instead of
 	                          sampling (tests), or IXG_MODE_AUTO */
@@ -73,6 +85,7 @@ IXG_HD static inline uint32_t ixg_fdir_hash(uint32_t src, uint32_t dst, uint32_t
 typedef struct ixg_kparams ixg_kparams;
 
 #define IXG_ZERO_PAGE 4096u
+#define IXG_PRESENT_WORDS 8u
 
 /* deferred chunk classes: SHORT = every frame shorter than 112 bytes (the
  * whole L4 segment lies in the 96-byte prefix + one 16-byte piece, no

@@ -959,7 +959,11 @@ constexpr int kModeLong = 0, kModeFirst = 2;
 // (Dn -> Pn) is loaded here, after this chunk's last streaming round is
 // issued (its registers free by then), instead of after this chunk, where
 // the next chunk waited out its whole latency
-template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false, bool DMX = true>
+// SPLIT (the parse kernel of the parse / tail split): no streaming rounds;
+// a long segment's pending sum, offsets and failure record go to p.tail for
+// the tail kernel, the record for a passing check is stored now, and the
+// chunk's tail mask to p.tmeta. Returns true when the chunk left tails.
+template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false, bool DMX = true, bool SPLIT = false>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x, const GDesc* Dn = nullptr,
                        GPre* Pn = nullptr) {
@@ -1001,6 +1005,7 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   const bool lng = !SHORT && strm && (pend > (uint32_t)kStreamBase || !short_tail);
   if (strm && !lng) s.l4_acc += piece_sum(v96, (int)rr);
   const uint64_t m = SHORT ? 0ull : __ballot(lng);
+  if (SPLIT && !m && lane == 0) p.tmeta[chunk] = 0ull;
   if (SHORT || !m) {  // no long segment in this chunk (wave-uniform)
     if (LATE) gen_pre<false, BIG>(p, *Dn, lane, *Pn);
     if (valid) {
@@ -1018,6 +1023,21 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   Rec rbad = make_record(p, d, L, s, 1u);
   uint32_t acc32 = fold32(s.l4_acc), ip_res = s.ip_res;
   uint32_t tsrc = s.src, tdst = s.dst, tports = s.ports;
+  if (SPLIT) {
+    if (lane == 0) p.tmeta[chunk] = m;
+    if (valid) {
+      if (lng) {
+        u32x4* t = reinterpret_cast<u32x4*>(p.tail) + 2u * (size_t)i;
+        t[0] = u32x4{(uint32_t)off, (uint32_t)(off >> 32), s.seg_end | (ip_res << 16), acc32};
+        t[1] = u32x4{rbad.w0, rbad.w1, rbad.w2, rbad.w3};
+        *reinterpret_cast<u32x4*>(p.out + i) = u32x4{rok.w0, rok.w1, rok.w2, rok.w3};  // (csum: the tail kernel)
+      } else {
+        store_record(p, i, rok, ip_res, r4);
+      }
+      store_demux<DMX>(p, i, rok, tsrc, tdst, tports);
+    }
+    return true;
+  }
   const u32x4 ve = load16(lng && rr != 0u, p.base + off + pend, p.zero + 16 * lane);
   // materialise these now, so the parse state (d[], s) is dead during the
   // streaming rounds instead of being kept live for sunk computations
@@ -1471,11 +1491,12 @@ ixg_rx_fastc_dmx_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false, bool BIG_OK = true, bool DMX = true>
+template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false, bool BIG_OK = true, bool DMX = true,
+          bool SPLIT = false>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
-  constexpr bool BIG = BIG_OK && MODE == kModeLong && !EARLY;
+  constexpr bool BIG = BIG_OK && MODE == kModeLong && (!EARLY || SPLIT);
   bool deferred = false;
   uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
   GDesc D1;
@@ -1489,7 +1510,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     GPre P1;
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     constexpr bool LATE = LATE_OK && !EARLY && MODE == kModeLong;
-    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE, DMX>(p, T, c0, lane, w, D0, P0, &D1, &P1);
+    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE, DMX, SPLIT>(p, T, c0, lane, w, D0, P0, &D1, &P1);
     if (!EARLY && !LATE) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
@@ -1506,7 +1527,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
 template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0, bool LATE = false, bool BIGOK = true,
-          int kWaves = 4, int kQGroups = 4, bool DMX = true>
+          int kWaves = 4, int kQGroups = 4, bool DMX = true, bool SPLIT = false>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -1572,6 +1593,8 @@ DEV void general_body(const KParams& p) {
     gen_desc<OFFS>(p, q[0], lane, D0);
     if (CLS == IXG_CLS_SHORT)
       seen |= gen_walk<OFFS, SEARLY, kModeFirst, 0, false, true, DMX>(p, T, w, q, nq, lane, D0);
+    else if (SPLIT)
+      seen |= gen_walk<OFFS, SEARLY, kModeLong, SM, false, BIGOK, DMX, true>(p, T, w, q, nq, lane, D0);
     else if (!SEARLY || wave_any(D0.L > (uint32_t)kStreamBase + 32u))
       gen_walk<OFFS, false, kModeLong, SM, LATE, BIGOK, DMX>(p, T, w, q, nq, lane, D0);
     else
@@ -1579,7 +1602,109 @@ DEV void general_body(const KParams& p) {
     __builtin_amdgcn_wave_barrier();
   }
   if (CLS == IXG_CLS_SHORT) publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
+  if (SPLIT && seen && lane == 0) p.present[4] = p.epoch;
 }
+
+#ifdef IXGRX_AB
+// ---- the tail kernel (the parse / tail split of the long class) -----------
+// A/B builds only: measured slower than the one-kernel general path (C3
+// 1.82 vs 1.49 ms per launch: parse 0.75 ms + tail 1.08 ms; C4 2.64 vs
+// 2.38 ms), see DESIGN.md section 8.
+// The parse kernel (general_body<SPLIT>) leaves each long L4 segment's whole
+// 16-byte pieces past the prefix in p.tail; this kernel streams them with
+// no parse state live (the streaming rounds of general_chunk: medium
+// segments by 4-lane groups, the rest by 16-lane groups, two rounds in
+// flight), so it runs at a higher occupancy than the one-kernel general
+// path, whose parse registers capped it at 2 waves per SIMD. Per chunk with
+// tails: the owners' items into the wave's LDS list, the rounds, then each
+// owner folds its sum; a failing check stores the failure record the parse
+// kernel built over the passing one (and its demux record).
+template <bool DMX>
+DEV void tail_chunk(const KParams& p, const WaveLds& w, uint32_t chunk, int lane) {
+  const uint64_t meta = p.tmeta[chunk];  // one address: a broadcast
+  const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(meta >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)meta);
+  const bool lng = (m >> lane) & 1u;
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const u32x4* t = reinterpret_cast<const u32x4*>(p.tail) + 2u * (size_t)i;
+  const u32x4 q0 = *(lng ? t : reinterpret_cast<const u32x4*>(p.zero));
+  const uint64_t off = ((uint64_t)q0.y << 32) | q0.x;
+  const uint32_t seg_end = q0.z & 0xffffu, ip_res = q0.z >> 16, acc = q0.w;
+  const uint32_t tl = seg_end - (uint32_t)kStreamBase, rr = tl & 15u, pend = (uint32_t)kStreamBase + (tl & ~15u);
+  const bool lmed = lng && pend <= (uint32_t)kStreamBase + kMedSpan;
+  const uint64_t mm = __ballot(lmed), mb = m & ~mm;
+  const uint32_t nmed = (uint32_t)__popcll(mm), nlong = (uint32_t)__popcll(m);
+  if (lng) {
+    const uint64_t mine = lmed ? mm : mb;
+    const uint32_t at = (lmed ? 0u : nmed) +
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+    w.list[at] = (uint32_t)lane;
+    w.end[lane] = pend;
+    w.offlo[lane] = (uint32_t)off;
+    w.offhi[lane] = (uint32_t)(off >> 32);
+  }
+  __builtin_amdgcn_wave_barrier();
+  const RoundPlan plan{nmed, nlong, (nmed + 64u / kMedG - 1u) / (64u / kMedG)};
+  const uint32_t R = plan.rm + (nlong - nmed + kRoundPk - 1) / kRoundPk;
+  const u32x4 ve = load16(lng && rr != 0u, p.base + off + pend, p.zero + 16 * lane);
+  Round A, B;
+  round_issue<1>(p, w, 0, plan, lane, A);
+#pragma clang loop unroll(disable)
+  for (uint32_t r = 0; r < R; r += 2) {
+    round_issue<1>(p, w, r + 1, plan, lane, B);
+    round_finish<1>(p, w, lane, A);
+    round_issue<1>(p, w, r + 2, plan, lane, A);
+    round_finish<1>(p, w, lane, B);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lng) {
+    const uint32_t res =
+        (~fold16(add1c(add1c(acc, w.sum[lane]), fold32(piece_sum(ve, (int)rr))))) & 0xffffu;
+    if (res != 0u) {
+      const u32x4 b = t[1];
+      *reinterpret_cast<u32x4*>(p.out + i) = b;
+      const Rec rb{b.x, b.y, b.z, b.w};
+      // (a failure record that is still IXG_V_TCP, IXG_F_NO_CSUM_DROP, has
+      // the passing record's lookup, stored by the parse kernel)
+      if (((b.x >> 16) & 0xffu) != IXG_V_TCP) store_demux<DMX>(p, i, rb, 0u, 0u, 0u);
+    }
+    if (p.csum) p.csum[i] = ip_res | (res << 16);
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int kTW, bool DMX>
+DEV void tail_body(const KParams& p) {
+  if (p.present[4] != p.epoch) return;  // the parse kernel left no tails
+  __shared__ uint32_t sh_list[kTW][64], sh_end[kTW][64], sh_offlo[kTW][64], sh_offhi[kTW][64], sh_sum[kTW][64],
+      sh_q[kTW][64];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * kTW;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t ngroups = (nchunks + 63u) >> 6;
+  const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
+                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), nullptr, nullptr};
+  lds_u32* q = LDS(lds_u32, sh_q[wave]);
+  // the chunks the parse kernel took (general_body's selection), of which
+  // those with tails
+  const bool all = launch_mode(p) == IXG_MODE_LONG;
+  for (uint32_t g = blockIdx.x * kTW + wave; g < ngroups; g += nw) {
+    const uint32_t ci = g * 64u + (uint32_t)lane;
+    const bool sel = ci < nchunks && (all || p.defer[ci] == IXG_CLS_LONG);
+    const bool want = sel && p.tmeta[sel ? ci : 0u] != 0ull;
+    const uint64_t m = __ballot(want);
+    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nq = (uint32_t)__popcll(m);
+    for (uint32_t j = 0; j < nq; j++) tail_chunk<DMX>(p, w, q[j], lane);
+  }
+}
+
+#define IXG_TAIL_KERNEL(NAME, WAVES, DMX)                                                           \
+  extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
+  NAME(KParams p) { tail_body<kWaves, DMX>(p); }
+IXG_TAIL_KERNEL(ixg_rx_tail, 4, true)
+#endif
 
 #define IXG_GEN_KERNEL(NAME, OFFS, CLS, WAVES, ...)                                                 \
   extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
@@ -1594,6 +1719,14 @@ DEV void general_body(const KParams& p) {
 // A/B, and C3's FETCH_SIZE 6.64 -> 6.53 GB)
 IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
 IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
+#ifdef IXGRX_AB
+// the parse kernel of the parse / tail split (ixg_rx_tail streams the tails)
+IXG_GEN_KERNEL(ixg_rx_parse_s, false, IXG_CLS_LONG, 3, true, 1, false, false, 4, 4, true, true)
+IXG_GEN_KERNEL(ixg_rx_parse_o, true, IXG_CLS_LONG, 3, true, 1, false, false, 4, 4, true, true)
+// 4 waves/SIMD without the one-ahead prefix prefetch
+IXG_GEN_KERNEL(ixg_rx_parse4_s, false, IXG_CLS_LONG, 4, false, 1, false, false, 4, 4, true, true)
+IXG_GEN_KERNEL(ixg_rx_parse4_o, true, IXG_CLS_LONG, 4, false, 1, false, false, 4, 4, true, true)
+#endif
 // the short-class general kernel (no streaming rounds): 4 waves/SIMD
 // without the one-ahead prefix prefetch (128 VGPRs; C5 -3% against the
 // 3-wave prefetching build)
@@ -2127,6 +2260,11 @@ static const ShortK k_short[] = {{{ixg_rx_short_sp_s, ixg_rx_short_sp_o}, 64 * k
                                  {{ixg_rx_short_cx0_s, ixg_rx_short_cx0_o}, 64 * kCxWaves}
 #endif
 };
+#ifdef IXGRX_AB
+// the parse kernel of the parse / tail split (A/B builds only)
+static const kern_fn k_parse[][2] = {{ixg_rx_parse_s, ixg_rx_parse_o}, {ixg_rx_parse4_s, ixg_rx_parse4_o}};
+static const int k_nparse = sizeof(k_parse) / sizeof(k_parse[0]);
+#endif
 static const int k_nshort = sizeof(k_short) / sizeof(k_short[0]);
 static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
 static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
@@ -2160,6 +2298,17 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
 extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
   int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff;
+#ifdef IXGRX_AB
+  // A/B builds: general variant 20 + k = the parse / tail split with parse
+  // variant k (with the defer flags)
+  bool split = false;
+  int pv = 0;
+  if (gv >= 20) {
+    split = true;
+    pv = gv - 20 < k_nparse ? gv - 20 : 0;
+    gv = 0;
+  }
+#endif
   if (gv >= k_ngen) gv = 0;
   if (sv >= k_nshort) sv = 0;
   const int lay = p.off ? 1 : 0;
@@ -2208,6 +2357,17 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
                        (hipStream_t)stream, p);
   }
+#ifdef IXGRX_AB
+  // the parse / tail split: the parse kernel, then the tail kernel over the
+  // tails it left (exits at once when none)
+  if (split && p.defer && p.tail) {
+    const kern_fn kp = k_parse[pv][lay];
+    hipLaunchKernelGGL(kp, dim3(grid_for(kp, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
+    hipLaunchKernelGGL(ixg_rx_tail, dim3(grid_for(ixg_rx_tail, group_blocks, ncu)), dim3(kBlock), 0,
+                       (hipStream_t)stream, p);
+    return (int)hipGetLastError();
+  }
+#endif
   const kern_fn kg = k_gen[gv][lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
   return (int)hipGetLastError();
