@@ -238,6 +238,19 @@ DEV uint32_t keep_bytes(uint32_t x, int t) {
   return x & ~(uint32_t)(~0ull << (8u * u));
 }
 
+// Bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L"). The
+// general parse loads prefixes raw (bytes past L belong to the next frame)
+// and masks only what can be consumed past L: every other field is read
+// behind a length check that already covers it (the IPv4 fields behind
+// ip.c:68's L >= 34, the L4 header and sums behind 14 + ip_len <= L, the
+// ports behind l4 + 4 <= L, the IPv6 fields behind L >= 54 / 54 + plen <=
+// L). Two are not: the Ethernet type of a frame shorter than 14 bytes, and
+// udp_input's length field (l4 + 4, unchecked by udp.c:59's own test).
+template <int N>
+DEV uint32_t eth_type(const uint32_t (&d)[N], uint32_t L) {
+  return ((L > 12u ? byte_at(d, 12) : 0u) << 8) | (L > 13u ? byte_at(d, 13) : 0u);
+}
+
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
@@ -270,7 +283,7 @@ template <int SHAPE, int NDW, class Tab, class T6P = const lds_u32*>
 DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixDw],
                     uint32_t L, LaneState& s, T6P T6 = nullptr) {
   constexpr bool FIXED = SHAPE == kShapeFixed;
-  const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);       // ip.c:132
+  const uint32_t etype = eth_type(d, L);                                   // ip.c:132
   const uint32_t vh = byte_at(d, 14);
   const uint32_t ver = vh >> 4;
   const int ihl = FIXED ? 5 : (int)(vh & 15u);                             // ip.h:84-90
@@ -433,7 +446,7 @@ DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixD
   s.seg_end = seg_end;
   s.doff = doff_byte >> 4;
   s.tcp_flags = tflags & 0x3fu;
-  s.ulen = bswap16(w45);
+  s.ulen = bswap16(keep_bytes(w45, (int)L - (int)s.l4 - 4));  // (udp_input reads it unchecked)
   s.icmp_type = b0;
 
   const uint32_t sp = s.proto;
@@ -495,7 +508,7 @@ DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixD
 template <bool FIXED = false>
 DEV Rec make_record(const KParams& p, const uint32_t (&d)[kPrefixDw], uint32_t L, const LaneState& s,
                     uint32_t l4_res) {
-  const uint32_t etype = FIXED ? 0x0800u : ((byte_at(d, 12) << 8) | byte_at(d, 13));
+  const uint32_t etype = FIXED ? 0x0800u : eth_type(d, L);
   const uint32_t vh = FIXED ? 0x45u : byte_at(d, 14);
   const uint32_t ver = vh >> 4, ihl = vh & 15u;
   const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
@@ -613,8 +626,8 @@ DEV uint64_t frame_off(const KParams& p, uint32_t i) {
 }
 
 // load 16-byte chunks [K0, K1) of the prefix; chunk k only if 16k < L.
-// Raw: the bytes at offsets >= L are zeroed by mask_prefix where the
-// prefix is consumed (a mask here would make the prefetch wait for its data)
+// Raw: bytes at offsets >= L are never consumed unmasked (eth_type and the
+// UDP length mask themselves; every other field sits behind a length check)
 template <int K0, int K1>
 DEV void load_prefix(const uint8_t* f, uint32_t L, const uint8_t* dummy, uint32_t (&d)[kPrefixDw]) {
   static_assert(K0 == 0, "prefix loads start at the frame start");
@@ -632,9 +645,11 @@ DEV void load_prefix(const uint8_t* f, uint32_t L, const uint8_t* dummy, uint32_
 }
 
 
-// Bytes at offsets >= L read as zero (DESIGN.md "bytes beyond L"). Only the
-// dwords at or past the wave's shortest frame can hold such bytes: the
-// others are left alone (one compare + a wave-uniform branch per dword).
+// Bytes at offsets >= L read as zero, every dword at or past the wave's
+// shortest frame masked (one compare + a wave-uniform branch per dword).
+// The parse masks the two fields that can be consumed past L (eth_type,
+// the UDP length), so the span kernel skips this (C5 -9 % in a
+// same-process A/B); the long kernel keeps it (C3 2-3 % faster with it).
 DEV void mask_prefix(uint32_t (&d)[kPrefixDw], uint32_t L) {
 #pragma unroll
   for (int j = 3; j < kPrefixDw; j++)
@@ -931,7 +946,7 @@ DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t ch
 #pragma unroll
   for (int j = 3; j < kPrefixDw; j++) d[j] = q[j];  // L >= 96: no masking
   LaneState s;
-  const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
+  const bool fixed = !valid || (eth_type(d, L) == 0x0800u && byte_at(d, 14) == 0x45u);
   if (wave_all(fixed))
     lane_parse<kShapeFixed, kPrefixDw>(p, Tab64{T}, d, L, s);
   else
@@ -985,11 +1000,13 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   uint32_t d[kPrefixDw];
 #pragma unroll
   for (int j = 0; j < kPrefixDw; j++) d[j] = x.d[j];
+  // (not needed for the results, eth_type and the UDP length mask
+  // themselves; but C3 measured 2-3 % faster with it in a same-process A/B)
   mask_prefix(d, L);
   const u32x4& v96 = x.v96;
   const bool short_tail = L > (uint32_t)kStreamBase && L < (uint32_t)kStreamBase + 32u;
   LaneState s;
-  const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
+  const bool fixed = !valid || (eth_type(d, L) == 0x0800u && byte_at(d, 14) == 0x45u);
   if (wave_all(fixed))
     lane_parse<kShapeFixed, kPrefixDw>(p, Tab64{T}, d, L, s);
   else
@@ -1363,7 +1380,6 @@ DEV void slow_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t c
   uint32_t d[kPrefixDw];
 #pragma unroll
   for (int k = 0; k < kPrefixDw; k++) d[k] = x.d[k];
-  mask_prefix(d, L);
   LaneState s;
   lane_parse<kShapeAny, kPrefixDw>(p, Tab64{T}, d, L, s, p.tab6);
   if (!valid) return;
@@ -1790,6 +1806,24 @@ DEV Span span_issue(const KParams& p, const GDesc& g, int lane, bool live, lds_u
   return sp;
 }
 
+// The lane parse specialised for the wave's header family (wave-uniform):
+// all IPv4 ihl 5 -> the constant geometry; no IPv6 lane -> no IPv6 code;
+// every lane IPv6 (IXG_F_IPV6) -> L4 at the constant 54, no IPv4 mux.
+template <class Tab>
+DEV void parse_dispatch(const KParams& p, const Tab& tab, const uint32_t (&d)[kPrefixDw], uint32_t L, bool valid,
+                        LaneState& st, const lds_u32* t6) {
+  const uint32_t et = eth_type(d, L);
+  const bool six = (p.flags & IXG_F_IPV6) && et == 0x86DDu;
+  if (wave_all(!valid || (et == 0x0800u && byte_at(d, 14) == 0x45u)))
+    lane_parse<kShapeFixed, kPrefixDw>(p, tab, d, L, st);
+  else if (wave_all(!valid || !six))
+    lane_parse<kShapeV4, kPrefixDw>(p, tab, d, L, st, t6);
+  else if (wave_all(!valid || six))
+    lane_parse<kShapeV6, kPrefixDw>(p, tab, d, L, st, t6);
+  else
+    lane_parse<kShapeAny, kPrefixDw>(p, tab, d, L, st, t6);
+}
+
 // AUX: the copies' cache policy (2 = nt)
 template <bool OFFS, bool DMX, int AUX = 0, bool STRIDED = true>
 DEV void short_span_body(const KParams& p) {
@@ -1894,13 +1928,8 @@ DEV void short_span_body(const KParams& p) {
       gen_desc<OFFS>(p, c2, lane, D2);
       // ---- parse chunk c0 ----
       if (live0) {
-        mask_prefix(d, L);
         LaneState st;
-        const bool fixed = !valid || (byte_at(d, 12) == 0x08u && byte_at(d, 13) == 0x00u && byte_at(d, 14) == 0x45u);
-        if (wave_all(fixed))
-          lane_parse<kShapeFixed, kPrefixDw>(p, tab, d, L, st);
-        else
-          lane_parse<kShapeAny, kPrefixDw>(p, tab, d, L, st, t6);
+        parse_dispatch(p, tab, d, L, valid, st, t6);
         // the 16-byte piece holding a segment end past byte 96 (frames < 112 B)
         if (valid && st.stream) st.l4_acc += piece_sum(v96, (int)(st.seg_end - (uint32_t)kStreamBase));
         if (valid) {
@@ -2193,27 +2222,43 @@ IXG_GEN_KERNEL(ixg_rx_general_w3nb_o, true, IXG_CLS_LONG, 3, false, 1, false, fa
 // half of them could be fixed-shape by length (every frame <= 64 B), else
 // SHORT when at least half are short, else LONG.
 extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
-  __shared__ uint32_t cnt[2];
+  __shared__ uint32_t cnt[kWaves][2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x < 2) cnt[threadIdx.x] = 0;
-  __syncthreads();
   const uint32_t nchunks = (p.n + 63u) >> 6;
   const uint32_t ns = nchunks < 64u ? nchunks : 64u;
-  uint32_t nf = 0, nsh = 0;
-  for (uint32_t k = (uint32_t)wave; k < ns; k += kWaves) {
-    const uint32_t c = (uint32_t)((uint64_t)k * nchunks / ns);
+  // every length load issued before the first vote (one round trip, not one
+  // per sample: the sampler is on every launch's critical path)
+  constexpr int kPer = 64 / kWaves;
+  uint32_t L[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const uint32_t k = (uint32_t)wave + (uint32_t)(kWaves * j);
+    const uint32_t c = ns ? k * nchunks / ns : 0u;  // k * nchunks < 64 * 2^26
     const uint32_t i = c * 64u + (uint32_t)lane;
-    const uint32_t L = i < p.n ? p.len[i] : 0u;
-    nf += wave_all(L <= 64u) ? 1u : 0u;
-    nsh += wave_all(L < IXG_SHORT_MAX) ? 1u : 0u;
+    const bool ok = k < ns && i < p.n;
+    const uint32_t v = p.len[ok ? i : 0u];
+    L[j] = ok ? v : 0u;
+  }
+  uint32_t nf = 0, nsh = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    if ((uint32_t)wave + (uint32_t)(kWaves * j) >= ns) break;
+    nf += wave_all(L[j] <= 64u) ? 1u : 0u;
+    nsh += wave_all(L[j] < IXG_SHORT_MAX) ? 1u : 0u;
   }
   if (lane == 0) {
-    atomicAdd(&cnt[0], nf);
-    atomicAdd(&cnt[1], nsh);
+    cnt[wave][0] = nf;
+    cnt[wave][1] = nsh;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t mode = 2 * cnt[0] >= ns ? IXG_MODE_FAST : (2 * cnt[1] >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
+    uint32_t f = 0, sh = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; w++) {
+      f += cnt[w][0];
+      sh += cnt[w][1];
+    }
+    uint32_t mode = 2 * f >= ns ? IXG_MODE_FAST : (2 * sh >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
     if (p.force_mode != IXG_MODE_AUTO) mode = p.force_mode;
     p.present[3] = mode;
     p.present[0] = p.epoch;
