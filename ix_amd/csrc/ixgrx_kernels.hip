@@ -1961,6 +1961,196 @@ IXG_SPAN_KERNEL(ixg_rx_short_spnt_s, false, false, 0, false)
 IXG_SPAN_KERNEL(ixg_rx_short_spnt_o, true, false, 0, false)
 #endif
 #ifdef IXGRX_AB
+// ---- the span-staged short kernel with cross-wave family compaction -------
+// A/B builds only (short variant 1): correct (the GPU suite passes with it
+// as the default) but slower than short_span_body: C5 0.548 vs 0.449 ms,
+// C5 reference semantics 0.506 vs 0.420, C5 in single-family runs 0.872 vs
+// 0.451 in a same-process A/B. The block barriers line the 16 waves up in
+// the same phase, so a step's copies, LDS traffic and parse no longer
+// overlap across waves, which costs more than the specialised parse saves.
+// C5's chunks mix IPv4 (with options) and IPv6 frames in every wave, so every
+// wave ran both the IPv4 header-length mux and hash and the IPv6 Toeplitz.
+// Here the 16 waves of a block each stage one chunk's span in LDS (as
+// short_span_body), then the block's frames are regrouped by header family
+// through LDS: IPv4 / non-IP frames take slots from 0 up, IPv6 frames
+// (IXG_F_IPV6) from 1023 down (one LDS atomic per wave and family), and wave
+// w parses slots [64 w, 64 w + 64) out of the spans of whichever waves hold
+// them. Every wave but the one at the boundary of a full block is then
+// single-family and takes the specialised parse (parse_dispatch). Records go
+// to the frames' own indices. A chunk that is not span-contiguous is parsed
+// by its own wave from per-lane loads. Three block barriers per step: slots
+// taken, spans read (then each wave issues its next chunk's copy), and the
+// step's parse overlaps those copies.
+template <bool OFFS, bool DMX>
+DEV void short_span_cx_body(const KParams& p) {
+  constexpr int W = kSpanWaves;
+  constexpr uint32_t kBuf = kSpanMax / 4 + 32;  // dwords per wave's span buffer
+  __shared__ uint64_t T[12 * 256];
+  __shared__ uint32_t sh_span[W][kBuf];
+  __shared__ uint32_t sh_q[W][64];
+  __shared__ uint32_t sh_desc[W * 64];  // per (wave, lane): dword index into sh_span | L << 16
+  __shared__ uint16_t sh_perm[W * 64];  // slot -> wave * 64 + lane
+  __shared__ uint32_t sh_chunk[W];      // each wave's chunk in this step
+  __shared__ uint32_t sh_nq[W];
+  __shared__ uint32_t sh_cnt[2][2];     // per step parity: IPv4 slots, IPv6 slots taken
+  extern __shared__ u32x4 dyn6[];       // IPv6 Toeplitz tables (IXG_F_IPV6)
+  static_assert(W * kBuf < 65536u, "span dword indices fit 16 bits");
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * W;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t mode = launch_mode(p);
+  const bool all = mode == IXG_MODE_SHORT;
+  if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
+  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
+  const uint32_t wv = blockIdx.x * W + wave, wv0 = blockIdx.x * W;
+  bool any = all;
+  for (uint32_t g = 0; !any && wv + 64u * g * nw < nchunks; g++) {
+    const uint32_t ci = wv + (64u * g + (uint32_t)lane) * nw;
+    any = wave_any(ci < nchunks && mine(ci));
+  }
+  if (!__syncthreads_or(any)) return;
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * W)
+      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
+  if (threadIdx.x < 4) sh_cnt[threadIdx.x >> 1][threadIdx.x & 1] = 0;
+  stage_tables(p, T);  // (ends with a block barrier)
+  const Tab64 tab{T};
+  const lds_u32* t6 = LDS(const lds_u32, dyn6);
+  lds_u32* buf = LDS(lds_u32, sh_span[wave]);
+  const lds_u32* spans = LDS(const lds_u32, &sh_span[0][0]);
+  lds_u32* q = LDS(lds_u32, sh_q[wave]);
+  bool seen = false;
+  uint32_t step = 0;
+  // chunk assignment as short_span_body (STRIDED); the loop bounds are the
+  // block's, every wave takes part in every barrier
+  for (uint32_t g0 = 0; wv0 + 64u * g0 * nw < nchunks; g0++) {
+    const uint32_t ci = wv + (64u * g0 + (uint32_t)lane) * nw;
+    const bool want = ci < nchunks && (all || mine(ci));
+    const uint64_t m = __ballot(want);
+    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+    const uint32_t nq = (uint32_t)__popcll(m);
+    if (lane == 0) sh_nq[wave] = nq;
+    __syncthreads();
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int w = 0; w < W; w++) nmax = sh_nq[w] > nmax ? sh_nq[w] : nmax;
+    __syncthreads();  // (sh_nq is rewritten by the next group)
+    if (nmax == 0) continue;
+    auto classify = [&](uint32_t chunk, GDesc& g) {
+      const bool defer = !wave_all(g.L < IXG_SHORT_MAX);  // (L = 0 past the batch end)
+      if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
+      seen |= defer;
+      if (defer) g.L = 0;
+      return !defer;
+    };
+    // a chunk whose frames are not one span of at most kSpanMax bytes goes
+    // to the long kernel (it takes any chunk)
+    auto stage = [&](uint32_t chunk, const GDesc& g, bool& live) {
+      const Span sp = span_issue<OFFS>(p, g, lane, live, buf);
+      if (live && sp.npc == 0u) {
+        if (lane == 0) p.defer[chunk] = (uint8_t)IXG_CLS_LONG;
+        seen = true;
+        live = false;
+      }
+      return sp;
+    };
+    uint32_t c0 = nq > 0 ? q[0] : kNoChunk;
+    GDesc D0, D1;
+    gen_desc<OFFS>(p, c0, lane, D0);
+    bool live0 = nq > 0 && classify(c0, D0);
+    Span S0 = stage(c0, D0, live0);
+    for (uint32_t j = 0; j < nmax; j++, step++) {
+      const uint32_t par = step & 1u;
+      // the next chunk's descriptors (needed after the second barrier)
+      const uint32_t c1 = j + 1 < nq ? q[j + 1] : kNoChunk;
+      gen_desc<OFFS>(p, c1, lane, D1);
+      // ---- this wave's chunk: its frames into the block's slots
+      const uint32_t i = c0 * 64u + (uint32_t)lane;
+      const bool valid = live0 && i < p.n;
+      const bool staged = S0.npc != 0;  // wave-uniform
+      const uint32_t L = D0.L;
+      uint32_t fam = 2u, w0 = 0u;  // 0: IPv4 / other, 1: IPv6, 2: not here
+      if (staged) {
+        __builtin_amdgcn_s_waitcnt(kGldsWait);
+        __builtin_amdgcn_wave_barrier();
+        w0 = (uint32_t)(D0.off - S0.base) >> 2;
+        const uint32_t dw3 = buf[L ? w0 + 3u : 0u];  // bytes 12..15
+        const uint32_t et = ((L > 12u ? dw3 & 0xffu : 0u) << 8) | (L > 13u ? (dw3 >> 8) & 0xffu : 0u);
+        fam = !valid ? 2u : (((p.flags & IXG_F_IPV6) && et == 0x86DDu) ? 1u : 0u);
+      }
+      const uint64_t b4 = __ballot(fam == 0u), b6 = __ballot(fam == 1u);
+      uint32_t base4 = 0, base6 = 0;
+      if (lane == 0) {
+        if (b4) base4 = atomicAdd(&sh_cnt[par][0], (uint32_t)__popcll(b4));
+        if (b6) base6 = atomicAdd(&sh_cnt[par][1], (uint32_t)__popcll(b6));
+      }
+      base4 = __builtin_amdgcn_readfirstlane(base4);
+      base6 = __builtin_amdgcn_readfirstlane(base6);
+      if (fam < 2u) {
+        const uint64_t bm = fam == 0u ? b4 : b6;
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        const uint32_t slot = fam == 0u ? base4 + r : (uint32_t)(W * 64 - 1) - (base6 + r);
+        sh_perm[slot] = (uint16_t)(wave * 64 + lane);
+      }
+      sh_desc[wave * 64 + lane] = ((uint32_t)wave * kBuf + w0) | (L << 16);
+      if (lane == 0) sh_chunk[wave] = c0;
+      __syncthreads();  // slots taken
+      const uint32_t n4 = sh_cnt[par][0], n6 = sh_cnt[par][1];
+      if (wave == 0 && lane < 2) sh_cnt[par ^ 1u][lane] = 0;  // the next step's (last read before this step)
+      // ---- slots [64 wave, 64 wave + 64): read the frames' prefixes
+      const uint32_t sl = (uint32_t)(wave * 64 + lane);
+      const bool have = sl < n4 || sl >= (uint32_t)(W * 64) - n6;
+      const uint32_t pd = have ? (uint32_t)sh_perm[sl] : 0u;
+      const uint32_t de = sh_desc[pd];
+      const uint32_t Ls = have ? de >> 16 : 0u;
+      const uint32_t is = sh_chunk[pd >> 6] * 64u + (pd & 63u);
+      uint32_t d[kPrefixDw];
+      u32x4 v96 = {0u, 0u, 0u, 0u};
+      {
+        const lds_u32* f = spans + (have ? (de & 0xffffu) : 0u);
+        d[0] = d[1] = d[2] = 0;
+#pragma unroll
+        for (int k = 3; k < kPrefixDw; k++) d[k] = f[k];
+        if (wave_any(Ls > (uint32_t)kStreamBase)) v96 = u32x4{f[24], f[25], f[26], f[27]};
+      }
+      __builtin_amdgcn_s_waitcnt(kLdsWait);
+      __syncthreads();  // every span read: the buffers may be refilled
+      bool live1 = false;
+      Span S1{0, 0};
+      if (j + 1 < nq) {
+        live1 = classify(c1, D1);
+        S1 = stage(c1, D1, live1);
+      }
+      // ---- parse the slots (single-family waves but at a full block's boundary)
+      if (wave_any(have)) {
+        LaneState st;
+        parse_dispatch(p, tab, d, Ls, have, st, t6);
+        if (have && st.stream) st.l4_acc += piece_sum(v96, (int)(st.seg_end - (uint32_t)kStreamBase));
+        if (have) {
+          const uint32_t r4 = l4_residual(st);
+          const Rec r = make_record(p, d, Ls, st, r4);
+          store_record(p, is, r, st.ip_res, r4);
+          store_demux<DMX>(p, is, r, st.src, st.dst, st.ports);
+        }
+      }
+      c0 = c1;
+      D0 = D1;
+      live0 = live1;
+      S0 = S1;
+    }
+  }
+  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
+}
+
+#define IXG_SPANCX_KERNEL(NAME, OFFS, DMX)                                                                     \
+  extern "C" __global__ void __launch_bounds__(64 * kSpanWaves) __attribute__((amdgpu_waves_per_eu(4))) \
+  NAME(KParams p) { short_span_cx_body<OFFS, DMX>(p); }
+IXG_SPANCX_KERNEL(ixg_rx_short_spx_s, false, false)
+IXG_SPANCX_KERNEL(ixg_rx_short_spx_o, true, false)
+#endif
+
+#ifdef IXGRX_AB
 IXG_GENW_KERNEL(ixg_rx_short_w10_s, 10, false, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
 IXG_GENW_KERNEL(ixg_rx_short_w10_o, 10, true, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
 #endif
@@ -2294,6 +2484,7 @@ struct ShortK {
 static const ShortK k_short_dmx = {{ixg_rx_short_w8d_s, ixg_rx_short_w8d_o}, 512};
 static const ShortK k_short[] = {{{ixg_rx_short_sp_s, ixg_rx_short_sp_o}, 64 * kSpanWaves}
 #ifdef IXGRX_AB
+                                 , {{ixg_rx_short_spx_s, ixg_rx_short_spx_o}, 64 * kSpanWaves}
                                  , {{ixg_rx_short_w8_s, ixg_rx_short_w8_o}, 512},
                                  {{ixg_rx_short_spnt_s, ixg_rx_short_spnt_o}, 64 * kSpanWaves}
                                  , {{ixg_rx_short_w10_s, ixg_rx_short_w10_o}, 640}
