@@ -11,12 +11,12 @@
 // A wave takes 64 segments. Pass A, one lane per segment: descriptor, header
 // dwords, IP checksum and the TCP pseudo-header term, into per-wave LDS.
 // Pass B, G lanes per segment (G = 4 when every frame of the 64 is at most
-// 96 bytes, else 16): lane t of a group writes output piece k = j + 3 (16
-// bytes at frame + 16k) for body piece j = G*r + t - 1 of round r. The
+// 96 bytes, else 16): lane t of a group loads body piece j = G*r + t of
+// round r and writes output piece k = j + 2 (16 bytes at frame + 16k). The
 // headers are 34 (TCP) or 42 (UDP) bytes, so every output piece is bytes
-// 14..15 (TCP) or 6..15 (UDP) of body piece j followed by the start of piece
-// j + 1 (from the next lane by a shuffle, or loaded by the group's last
-// lane); "body piece -1" is the header's last 16 bytes. Loads are aligned
+// 14..15 (TCP) or 6..15 (UDP) of body piece j - 1 (the previous lane's, by
+// a shuffle) followed by the start of piece j; "body piece -1" is the
+// header's last 16 bytes. Loads are aligned
 // to the segment start (4-byte aligned), stores to the frame start (16-byte
 // aligned). TCP's body sum is reduced across the group and patched into
 // output piece 3 (frame bytes 48..63, the checksum at 50..51) last.
@@ -206,14 +206,23 @@ DEV void store16(uint64_t addr, const u32x4& v) { *reinterpret_cast<u32x4*>(addr
 // rate, so that path keeps default-policy stores)
 DEV void store16_nt(uint64_t addr, const u32x4& v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(addr)); }
 
-// rounds in flight in the streaming pass: 3 -> 1514-B frames 3.02 -> 2.89 ms
-// per 4M (same-process A/B), echo replies unchanged; 4 spills at 128 VGPRs
+// rounds in flight in the streaming pass (one 16-byte load per lane and
+// round): 5 ran 1514-B frames 7 % slower than 3 in a same-process A/B
 #ifndef IXG_TX_RIF
 #define IXG_TX_RIF 3
 #endif
 constexpr int kTxRif = IXG_TX_RIF;
 
-// Pass B: G lanes per segment, 64 / G segments at a time.
+// Pass B: G lanes per segment, 64 / G segments at a time. Lane t of round r
+// loads body piece j = G r + t (aligned to the segment) and writes output
+// piece k = j + 2: bytes 14..15 (TCP) / 6..15 (UDP) of piece j - 1, then the
+// start of piece j. Piece j - 1 is the previous lane's (a shuffle), for the
+// group's first lane the previous round's last lane's (kept from that round),
+// and before round 0 the header's last 16 bytes: every load is the lane's
+// own piece (an earlier build also loaded piece j + 1 in the group's last
+// lane: twice the loads and registers per round). TCP's sum (each lane sums
+// its own piece) is reduced across the group and patched into output piece 3
+// (frame bytes 48..63, the checksum at 50..51), stored last.
 template <int G>
 DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
   const int g = lane / G, t = lane % G;
@@ -230,39 +239,39 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
     uint32_t hp[5];
 #pragma unroll
     for (int k = 0; k < 5; k++) hp[k] = w.hdr[(hb + k) * 64 + si];
-    const u32x4 pm1 = {mid(hp[0], hp[1]), mid(hp[1], hp[2]), mid(hp[2], hp[3]), mid(hp[3], hp[4])};
+    u32x4 carry = {mid(hp[0], hp[1]), mid(hp[1], hp[2]), mid(hp[2], hp[3]), mid(hp[3], hp[4])};
     const int nr = valid ? (K - 2 + G - 1) / G : 0;  // output pieces 2..K-1
     uint64_t acc = 0;
     u32x4 held = {0u, 0u, 0u, 0u};
     const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
     // always-issued loads (the zero page when there is nothing to read)
-    auto issue = [&](int r, u32x4& v, u32x4& vn) {
-      const bool act = r < nr;
-      const int j = G * r + t - 1;
-      const bool lo = act && j >= 0, ln = act && t == G - 1;
-      v = *reinterpret_cast<const u32x4_a4*>(lo ? src + 16u * (uint32_t)j : zero);
-      vn = *reinterpret_cast<const u32x4_a4*>(ln ? src + 16u * (uint32_t)(j + 1) : zero);
+    auto issue = [&](int r) {
+      const int j = G * r + t;
+      const bool act = r < nr && j + 2 < K;
+      return *reinterpret_cast<const u32x4_a4*>(act ? src + 16u * (uint32_t)j : zero);
     };
-    auto round = [&](int r, const u32x4& v, const u32x4& vn) {
-      const bool act = r < nr;
-      const int j = G * r + t - 1;
-      const u32x4 own = j < 0 ? pm1 : v;
-      u32x4 nxt;
-      nxt.x = (uint32_t)__shfl_down((int)own.x, 1, G);
-      nxt.y = (uint32_t)__shfl_down((int)own.y, 1, G);
-      nxt.z = (uint32_t)__shfl_down((int)own.z, 1, G);
-      nxt.w = (uint32_t)__shfl_down((int)own.w, 1, G);
-      if (t == G - 1) nxt = vn;
-      // output piece k = j + 3: bytes 14..15 (TCP) / 6..15 (UDP) of own,
-      // then the start of nxt
+    auto round = [&](int r, const u32x4& own) {
+      const int j = G * r + t;
+      const bool act = r < nr && j + 2 < K;
+      u32x4 prev;
+      prev.x = (uint32_t)__shfl_up((int)own.x, 1, G);
+      prev.y = (uint32_t)__shfl_up((int)own.y, 1, G);
+      prev.z = (uint32_t)__shfl_up((int)own.z, 1, G);
+      prev.w = (uint32_t)__shfl_up((int)own.w, 1, G);
+      if (t == 0) prev = carry;
+      // the group's last piece of this round: the next round's first lane's prev
+      carry.x = (uint32_t)__shfl((int)own.x, G - 1, G);
+      carry.y = (uint32_t)__shfl((int)own.y, G - 1, G);
+      carry.z = (uint32_t)__shfl((int)own.z, G - 1, G);
+      carry.w = (uint32_t)__shfl((int)own.w, G - 1, G);
       u32x4 o;
       if (udp) {
-        o = {mid(own.y, own.z), mid(own.z, own.w), mid(own.w, nxt.x), mid(nxt.x, nxt.y)};
+        o = {mid(prev.y, prev.z), mid(prev.z, prev.w), mid(prev.w, own.x), mid(own.x, own.y)};
       } else {
-        o = {mid(own.w, nxt.x), mid(nxt.x, nxt.y), mid(nxt.y, nxt.z), mid(nxt.z, nxt.w)};
+        o = {mid(prev.w, own.x), mid(own.x, own.y), mid(own.y, own.z), mid(own.z, own.w)};
       }
-      const int k = j + 3;
-      if (act && k < K) {
+      const int k = j + 2;
+      if (act) {
         if (!udp && k == 3)
           held = o;  // holds the TCP checksum: stored after the reduction
         else
@@ -272,21 +281,21 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
         store16(out, u32x4{w.hdr[0 * 64 + si], w.hdr[1 * 64 + si], w.hdr[2 * 64 + si], w.hdr[3 * 64 + si]});
         store16(out + 16u, u32x4{w.hdr[4 * 64 + si], w.hdr[5 * 64 + si], w.hdr[6 * 64 + si], w.hdr[7 * 64 + si]});
       }
-      // body piece j + 1 is summed by the lane it is `nxt` for: pieces
-      // 0..K-3 are, which covers the segment (K - 2 >= ceil(seg_len / 16))
+      // each lane sums its own body piece: pieces 0..K-3 cover the segment
+      // (K - 2 >= ceil(seg_len / 16))
       if (full && act) {
-        u32x4 sv = nxt;
-        if (j == 0) sv.x &= 0xffff0000u;  // the checksum field (segment bytes 16..17) counts as 0
-        acc += piece_sum(sv, seg_len - 16 * (j + 1));
+        u32x4 sv = own;
+        if (j == 1) sv.x &= 0xffff0000u;  // the checksum field (segment bytes 16..17) counts as 0
+        acc += piece_sum(sv, seg_len - 16 * j);
       }
     };
     // kTxRif rounds' loads in flight per lane
     for (int r = 0; __any(r < nr); r += kTxRif) {
-      u32x4 v[kTxRif], n[kTxRif];
+      u32x4 v[kTxRif];
 #pragma unroll
-      for (int q = 0; q < kTxRif; q++) issue(r + q, v[q], n[q]);
+      for (int q = 0; q < kTxRif; q++) v[q] = issue(r + q);
 #pragma unroll
-      for (int q = 0; q < kTxRif; q++) round(r + q, v[q], n[q]);
+      for (int q = 0; q < kTxRif; q++) round(r + q, v[q]);
     }
     if (!udp) {
 #pragma unroll
