@@ -16,10 +16,10 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt
 python3 tools/kt_summary.py "$O/kt" > "$O/launch_summary.md" || exit 1
 du -sh "$O"/* ; find "$O" -size +1M -exec ls -la {} \;
 SPECS=""
-for W in c2 c4 c3 c5; do
+for W in c2 c4 c3 c5 c5r; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_${W}_$C" -o p -- python3 bench.py --workload $W \
-      --secondary '' --no-cpu --no-copy --no-demux --no-tx --no-bad --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
+      --secondary '' --no-cpu --no-copy --no-demux --no-tx --no-bad --no-strong --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
       || { echo "pmc $W $C failed"; tail -20 "$O/pmc_${W}_$C.log"; exit 1; }
     find "$O/pmc_${W}_$C" -type f -exec ls -la {} \;
     [ -n "$(find "$O/pmc_${W}_$C" -name '*counter_collection.csv')" ] || { echo "no csv: $W $C"; tail -30 "$O/pmc_${W}_$C.log"; find "$O" -size +1M -delete; exit 1; }
@@ -30,4 +30,5 @@ find "$O" -size +8M -exec ls -la {} \; -delete
 python3 tools/pmc_traffic.py "$O/traffic.json" $SPECS || exit 1
 mkdir -p profiles && cp "$O/traffic.json" profiles/traffic.json
 timeout -k 10 400 python3 $B > "$O/bench.json" 2> "$O/bench.log" || { echo "bench failed"; tail -20 "$O/bench.log"; exit 1; }
+timeout -k 10 120 python3 tools/copy_probe.py > "$O/copy_probe.txt" 2>&1 || exit 1
 cat "$O/bench.json"
