@@ -849,9 +849,14 @@ def main():
         wl = None
         torch.cuda.empty_cache()
 
+        # one batch, one configuration: every rank's slice is processed as
+        # the same device's frames (dev_idx 0), whatever the rank
+        seng = ixgrx.RxEngine(ixgrx.Config(key, 128, 0, 0), device=local)
+
         def run_slice(blob, lens, S, m, out, stream):
-            engine(0).batch_dev(blob.data_ptr(), None, lens.data_ptr(), S, m, out.data_ptr(), None, stream)
+            seng.batch_dev(blob.data_ptr(), None, lens.data_ptr(), S, m, out.data_ptr(), None, stream)
         res["c4_strong"], schk = strong_leg(dev, run_slice, dist, world, rank, n_total=args.strong_n)
+        seng.close()
         if schk:
             checks.append(schk)
         torch.cuda.empty_cache()
