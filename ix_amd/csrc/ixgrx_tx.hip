@@ -207,11 +207,20 @@ DEV void store16(uint64_t addr, const u32x4& v) { *reinterpret_cast<u32x4*>(addr
 DEV void store16_nt(uint64_t addr, const u32x4& v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(addr)); }
 
 // rounds in flight in the streaming pass (one 16-byte load per lane and
-// round): 5 ran 1514-B frames 7 % slower than 3 in a same-process A/B
+// round): 6 = every round of a 1514-B frame's 16-lane group at once;
+// 1514-B frames -7 %, mixed -2.5 % against 3 (and 5 slower than 3) in a
+// same-process A/B
 #ifndef IXG_TX_RIF
-#define IXG_TX_RIF 3
+#define IXG_TX_RIF 6
 #endif
 constexpr int kTxRif = IXG_TX_RIF;
+
+// lane t - 1's value within groups of G lanes (lane 0: lane G - 1's)
+template <int G>
+DEV uint32_t rot1(uint32_t v) {
+  static_assert(G == 16 || G == 4, "DPP rotations within rows of 16 or quads");
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, G == 16 ? 0x121 : 0x93, 0xf, 0xf, false);
+}
 
 // Pass B: G lanes per segment, 64 / G segments at a time. Lane t of round r
 // loads body piece j = G r + t (aligned to the segment) and writes output
@@ -253,17 +262,13 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
     auto round = [&](int r, const u32x4& own) {
       const int j = G * r + t;
       const bool act = r < nr && j + 2 < K;
-      u32x4 prev;
-      prev.x = (uint32_t)__shfl_up((int)own.x, 1, G);
-      prev.y = (uint32_t)__shfl_up((int)own.y, 1, G);
-      prev.z = (uint32_t)__shfl_up((int)own.z, 1, G);
-      prev.w = (uint32_t)__shfl_up((int)own.w, 1, G);
-      if (t == 0) prev = carry;
-      // the group's last piece of this round: the next round's first lane's prev
-      carry.x = (uint32_t)__shfl((int)own.x, G - 1, G);
-      carry.y = (uint32_t)__shfl((int)own.y, G - 1, G);
-      carry.z = (uint32_t)__shfl((int)own.z, G - 1, G);
-      carry.w = (uint32_t)__shfl((int)own.w, G - 1, G);
+      // rotate the group's pieces by one lane (DPP row_ror:1 for 16-lane
+      // groups, quad_perm [3,0,1,2] for 4-lane ones): lane t gets lane
+      // t - 1's piece, lane 0 its group's last lane's, which is the next
+      // round's lane-0 predecessor
+      const u32x4 rot = {rot1<G>(own.x), rot1<G>(own.y), rot1<G>(own.z), rot1<G>(own.w)};
+      const u32x4 prev = t == 0 ? carry : rot;
+      carry = rot;
       u32x4 o;
       if (udp) {
         o = {mid(prev.y, prev.z), mid(prev.z, prev.w), mid(prev.w, own.x), mid(own.x, own.y)};
@@ -286,7 +291,11 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
       if (full && act) {
         u32x4 sv = own;
         if (j == 1) sv.x &= 0xffff0000u;  // the checksum field (segment bytes 16..17) counts as 0
-        acc += piece_sum(sv, seg_len - 16 * j);
+        const int rem = seg_len - 16 * j;
+        if (__all(!act || rem >= 16))
+          acc += (uint64_t)sv.x + sv.y + sv.z + sv.w;
+        else
+          acc += piece_sum(sv, rem);
       }
     };
     // kTxRif rounds' loads in flight per lane
@@ -371,67 +380,45 @@ DEV void tx_small(const TParams& p, const Seg& sg, const u32x4& b0, const u32x4&
   }
 }
 
-DEV void tx_loop(const TParams& p, const WaveTx& w) {
+// One chunk of 64 segments per wave (the grid has a wave per chunk: see
+// ixgrx_tx_launch), so no loads are carried across chunks.
+DEV void tx_chunk(const TParams& p, const WaveTx& w) {
   const int lane = threadIdx.x & 63;
-  const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (c >= nchunks) return;
-  // software pipeline: descriptors two chunks ahead, MACs and small
-  // segments' bytes one chunk ahead. A chunk the streaming pass takes issues
-  // the next loads only after it, so they do not hold registers across it.
-  TDesc d0 = tx_desc(p, c * 64u + (uint32_t)lane), d1 = tx_desc(p, (c + (uint64_t)nw) * 64u + (uint32_t)lane);
+  const uint32_t i = c * 64u + (uint32_t)lane;
+  const TDesc d0 = tx_desc(p, i);
   TPre x0;
-  tx_pre(p, c * 64u + (uint32_t)lane, d0, lane, x0);
-  for (;; c += nw) {
-    const uint32_t i = c * 64u + (uint32_t)lane;
-    const uint64_t i1 = i + 64ull * nw;
-    const bool last = c + nw >= nchunks;
-    uint32_t K0;
-    tx_valid(p, i, d0, K0);
-    if (__all(K0 <= 4u)) {
-      const TDesc d2 = tx_desc(p, i1 + 64ull * nw);
-      TPre x1;
-      tx_pre(p, i1, d1, lane, x1);
-      const Seg sg = tx_prepare(p, i, d0, x0);
-      tx_small(p, sg, x0.b0, x0.b1, lane, w.src_lo);
-      d0 = d1;
-      d1 = d2;
-      x0 = x1;
-    } else {
-      const Seg sg = tx_prepare(p, i, d0, x0);
-      const uint32_t K = sg.K;
-      tx_publish(sg, lane, w);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (__all(K <= 6u))
-        tx_stream<4>(p, lane, w);
-      else
-        tx_stream<16>(p, lane, w);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      const TDesc d2 = tx_desc(p, i1 + 64ull * nw);
-      TPre x1;
-      tx_pre(p, i1, d1, lane, x1);
-      d0 = d1;
-      d1 = d2;
-      x0 = x1;
-    }
-    if (last) break;
+  tx_pre(p, i, d0, lane, x0);
+  uint32_t K0;
+  tx_valid(p, i, d0, K0);
+  const Seg sg = tx_prepare(p, i, d0, x0);
+  if (__all(K0 <= 4u)) {
+    tx_small(p, sg, x0.b0, x0.b1, lane, w.src_lo);
+    return;
   }
+  tx_publish(sg, lane, w);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (__all(sg.K <= 6u))
+    tx_stream<4>(p, lane, w);
+  else
+    tx_stream<16>(p, lane, w);
 }
 
 }  // namespace
 
-// 4 waves per SIMD: at the 132 VGPRs the pipeline would otherwise take (3
-// waves), mixed-size batches ran 11% slower
-extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) ixg_tx_build(TParams p) {
+#ifndef IXG_TX_WAVES
+#define IXG_TX_WAVES 5
+#endif
+extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IXG_TX_WAVES)))
+ixg_tx_build(TParams p) {
   __shared__ uint32_t sh[kWaves][(7 + kHdr) * 64];
   lds_u32* b = (lds_u32*)sh[threadIdx.x >> 6];
   const WaveTx w{b, b + 64, b + 128, b + 192, b + 256, b + 320, b + 384, b + 448};
-  tx_loop(p, w);
+  tx_chunk(p, w);
 }
 
 extern "C" int ixgrx_tx_launch(const void* params, uint32_t ncu, void* stream) {
@@ -441,7 +428,11 @@ extern "C" int ixgrx_tx_launch(const void* params, uint32_t ncu, void* stream) {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, ixg_tx_build, kBlock, 0) != hipSuccess || nb < 1) nb = 1;
   const uint64_t cap = (uint64_t)ncu * (uint64_t)nb;
-  const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+  // one wave per chunk, not a persistent grid: 1514-B frames -1.5 %, mixed
+  // sizes -13 %, echo replies -8 % in a same-process A/B (the dispatcher
+  // keeps every CU fed; a plain copy behaves the same, tools/probe_copy.hip)
+  (void)cap;
+  const uint32_t grid = (uint32_t)want;
   hipLaunchKernelGGL(ixg_tx_build, dim3(grid ? grid : 1u), dim3(kBlock), 0, (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
