@@ -206,10 +206,11 @@ DEV void store16(uint64_t addr, const u32x4& v) { *reinterpret_cast<u32x4*>(addr
 // rate, so that path keeps default-policy stores)
 DEV void store16_nt(uint64_t addr, const u32x4& v) { __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(addr)); }
 
-// rounds in flight in the streaming pass (one 16-byte load per lane and
-// round): 6 = every round of a 1514-B frame's 16-lane group at once;
-// 1514-B frames -7 %, mixed -2.5 % against 3 (and 5 slower than 3) in a
-// same-process A/B
+// rounds in flight per segment group in the streaming pass (one 16-byte
+// load per lane and round): 6 = every round of a 1514-B frame's 16-lane
+// group at once (1514-B frames -7 %, mixed -2.5 % against 3 in a
+// same-process A/B); the next group's are issued before this group's are
+// consumed (tx_stream), a further -9 % on 1514-B and mixed frames
 #ifndef IXG_TX_RIF
 #define IXG_TX_RIF 6
 #endif
@@ -235,8 +236,31 @@ DEV uint32_t rot1(uint32_t v) {
 template <int G>
 DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
   const int g = lane / G, t = lane % G;
+  const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
+  // the first kTxRif rounds' loads of segment si (always issued: the zero
+  // page when there is nothing to read)
+  auto first_loads = [&](int si, u32x4 (&v)[kTxRif]) {
+    const uint32_t meta = w.meta[si];
+    const int K = (int)(meta & 0xffffu);
+    const int nr = ((meta >> 17) & 1u) ? (K - 2 + G - 1) / G : 0;
+    const uint64_t src = ((uint64_t)w.src_hi[si] << 32) | w.src_lo[si];
+#pragma unroll
+    for (int q = 0; q < kTxRif; q++) {
+      const int j = G * q + t;
+      const bool act = q < nr && j + 2 < K;
+      v[q] = *reinterpret_cast<const u32x4_a4*>(act ? src + 16u * (uint32_t)j : zero);
+    }
+  };
+  // software pipeline over the segment groups: the next group's first
+  // rounds are in flight while this group's are shifted and stored
+  u32x4 nxt[kTxRif];
+  first_loads(g, nxt);
   for (int s0 = 0; s0 < 64; s0 += 64 / G) {
     const int si = s0 + g;
+    u32x4 cur[kTxRif];
+#pragma unroll
+    for (int q = 0; q < kTxRif; q++) cur[q] = nxt[q];
+    if (s0 + 64 / G < 64) first_loads(si + 64 / G, nxt);
     const uint32_t meta = w.meta[si];
     const bool valid = (meta >> 17) & 1u, udp = (meta >> 16) & 1u, full = (meta >> 18) & 1u;
     const int K = (int)(meta & 0xffffu);
@@ -252,7 +276,6 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
     const int nr = valid ? (K - 2 + G - 1) / G : 0;  // output pieces 2..K-1
     uint64_t acc = 0;
     u32x4 held = {0u, 0u, 0u, 0u};
-    const uint64_t zero = reinterpret_cast<uint64_t>(p.zero) + 16u * (uint32_t)lane;
     // always-issued loads (the zero page when there is nothing to read)
     auto issue = [&](int r) {
       const int j = G * r + t;
@@ -298,13 +321,13 @@ DEV void tx_stream(const TParams& p, int lane, const WaveTx& w) {
           acc += piece_sum(sv, rem);
       }
     };
-    // kTxRif rounds' loads in flight per lane
-    for (int r = 0; __any(r < nr); r += kTxRif) {
-      u32x4 v[kTxRif];
 #pragma unroll
-      for (int q = 0; q < kTxRif; q++) v[q] = issue(r + q);
-#pragma unroll
-      for (int q = 0; q < kTxRif; q++) round(r + q, v[q]);
+    for (int q = 0; q < kTxRif; q++) round(q, cur[q]);
+    // segments longer than kTxRif rounds (not IX's MTU-sized ones): the
+    // rest, one round at a time
+    for (int r = kTxRif; __any(r < nr); r++) {
+      const u32x4 v = issue(r);
+      round(r, v);
     }
     if (!udp) {
 #pragma unroll
@@ -410,8 +433,10 @@ DEV void tx_chunk(const TParams& p, const WaveTx& w) {
 
 }  // namespace
 
+// 3 waves/SIMD (161 VGPRs: two groups' rounds in registers); at 4 or 5 the
+// pipelined streaming pass spills
 #ifndef IXG_TX_WAVES
-#define IXG_TX_WAVES 5
+#define IXG_TX_WAVES 3
 #endif
 extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(IXG_TX_WAVES)))
 ixg_tx_build(TParams p) {
