@@ -109,6 +109,23 @@ def _p2p(ops, dist) -> None:
             w.wait()
 
 
+# the largest single send/recv: a slice of C4's 64M-frame batch is 12.7 GB
+# at N = 8; transfers go out as <= 1 GiB pieces in the same group (message
+# counts stay far from 2^31 in every library on the path)
+P2P_MAX_BYTES = 1 << 30
+
+
+def _pieces(t, max_bytes: int | None = None):
+    """`t` split along dim 0 into views of at most max_bytes (default
+    P2P_MAX_BYTES; sender and receiver split same-shaped tensors
+    identically)."""
+    if max_bytes is None:
+        max_bytes = P2P_MAX_BYTES
+    row = t.element_size() * (int(np.prod(t.shape[1:])) if t.dim() > 1 else 1)
+    step = max(1, max_bytes // row)
+    return [t[k:k + step] for k in range(0, t.shape[0], step)]
+
+
 def _host_staged(dist, t) -> bool:
     """gloo moves host tensors only: device tensors are staged through host
     memory (the CPU rehearsal of the split; RCCL sends HBM to HBM)."""
@@ -120,8 +137,9 @@ def scatter_frames(blob, lens, stride: int, bounds, dist, device, src: int = 0):
     `src` holds the whole batch (`blob`: n * stride frame bytes + TAIL_PAD,
     `lens`: n int16 lengths; None on the other ranks) and every other rank r
     receives frames [s_r, e_r) of `bounds` (shard_bounds: unequal slices are
-    fine). One grouped send/recv per peer (RCCL batches them into one group,
-    so the slices leave GPU `src` over their own xGMI links at once).
+    fine). Grouped send/recv per peer, in pieces of at most P2P_MAX_BYTES
+    (RCCL batches them into one group, so the slices leave GPU `src` over
+    their own xGMI links at once).
 
     Returns this rank's (blob, lens) on `device`, ready for ixg_rx_batch_dev:
     on `src` they are views into the batch (the frames after the slice, or
@@ -143,7 +161,7 @@ def scatter_frames(blob, lens, stride: int, bounds, dist, device, src: int = 0):
             fb, lb = blob[a * stride:b * stride], lens[a:b]
             if _host_staged(dist, fb):
                 fb, lb = fb.cpu(), lb.cpu()
-            ops += [P(dist.isend, fb, r), P(dist.isend, lb, r)]
+            ops += [P(dist.isend, x, r) for x in _pieces(fb)] + [P(dist.isend, lb, r)]
         _p2p(ops, dist)
         return blob[s * stride:], lens[s:e]
     out_blob = torch.zeros(m * stride + TAIL_PAD, dtype=torch.uint8, device=device)
@@ -153,7 +171,7 @@ def scatter_frames(blob, lens, stride: int, bounds, dist, device, src: int = 0):
         staged = _host_staged(dist, rb)
         if staged:
             rb, rl = torch.empty(m * stride, dtype=torch.uint8), torch.empty(m, dtype=torch.int16)
-        _p2p([P(dist.irecv, rb, src), P(dist.irecv, rl, src)], dist)
+        _p2p([P(dist.irecv, x, src) for x in _pieces(rb)] + [P(dist.irecv, rl, src)], dist)
         if staged:
             out_blob[:m * stride].copy_(rb)
             out_lens.copy_(rl)
@@ -172,7 +190,7 @@ def gather_frame_records(rec, bounds, dist, out=None, dst: int = 0):
     if rank != dst:
         if rec.shape[0]:
             t = rec.cpu() if _host_staged(dist, rec) else rec
-            _p2p([P(dist.isend, t, dst)], dist)
+            _p2p([P(dist.isend, x, dst) for x in _pieces(t)], dist)
         return None
     s, e = bounds[rank]
     if e > s and rec.data_ptr() != out[s:e].data_ptr():
@@ -185,7 +203,7 @@ def gather_frame_records(rec, bounds, dist, out=None, dst: int = 0):
         if _host_staged(dist, t):
             t = torch.empty((b - a, 16), dtype=torch.uint8)
             staged.append((a, b, t))
-        ops.append(P(dist.irecv, t, r))
+        ops += [P(dist.irecv, x, r) for x in _pieces(t)]
     _p2p(ops, dist)
     for a, b, t in staged:
         out[a:b].copy_(t)

@@ -24,6 +24,8 @@ def main():
     kind, n, eng = os.environ["IXT_KIND"], int(os.environ["IXT_N"]), os.environ["IXT_ENGINE"]
     dist.init_process_group("gloo", rank=rank, world_size=world)
     if kind == "strong":
+        # small transfer pieces: every slice goes out as many sends
+        shard.P2P_MAX_BYTES = int(os.environ.get("IXT_P2P_MAX", shard.P2P_MAX_BYTES))
         ok = strong(rank, world, n, eng)
         dist.barrier()
         dist.destroy_process_group()

@@ -20,12 +20,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, kind, n, engine, timeout=300):
+def _run(world, kind, n, engine, timeout=300, **extra):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), IXT_KIND=kind, IXT_N=str(n), IXT_ENGINE=engine)
+                   MASTER_PORT=str(port), IXT_KIND=kind, IXT_N=str(n), IXT_ENGINE=engine, **extra)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "multi_worker.py")], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -57,8 +57,9 @@ def test_two_ranks_gloo_hip(kind, n):
 def test_strong_split_gloo(world, n):
     """bench.py's C4 line (one batch on rank 0, split by shard_bounds,
     scattered, processed, records gathered) end to end over gloo; world 3
-    gives unequal slices."""
-    _run(world, "strong", n, "oracle")
+    gives unequal slices; transfers in 100 000-byte pieces (many per slice,
+    the last one partial)."""
+    _run(world, "strong", n, "oracle", IXT_P2P_MAX="100000")
 
 
 @pytest.mark.gpu
@@ -94,3 +95,16 @@ def test_shard_trace_frames_identical():
             for i in (0, part.n // 2, part.n - 1):
                 assert part.frame(i) == tr.frame(s + i)
             assert part.blob.shape[0] >= int(part.offsets()[-1]) + int(part.len[-1]) + traces.TAIL_PAD
+
+
+def test_p2p_pieces_cover_in_order():
+    """Transfers split into <= P2P_MAX_BYTES views that tile the tensor in
+    order, the same way on both ends."""
+    import torch
+    t = torch.arange(10 * 16, dtype=torch.uint8).view(10, 16)
+    ps = shard._pieces(t, 48)
+    assert [p.shape[0] for p in ps] == [3, 3, 3, 1]
+    assert torch.equal(torch.cat(ps), t)
+    b = torch.arange(100, dtype=torch.uint8)
+    assert [p.numel() for p in shard._pieces(b, 30)] == [30, 30, 30, 10]
+    assert len(shard._pieces(torch.empty(0, dtype=torch.uint8), 30)) == 0
