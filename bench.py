@@ -140,26 +140,35 @@ class Workload:
 
 
 def time_steps(wl, eng, steps, warmup, dist, world):
+    """W warm-up launches, then exactly K timed launches back to back
+    (barrier + synchronize on both sides; the wall time, max over ranks, is
+    the line's value), then the same K launches again, each between HIP
+    events on the launch stream, for the per-launch kernel time the
+    roofline uses (events between launches would add their own gaps to the
+    value loop)."""
     import torch
     stream = torch.cuda.current_stream()
     sp = stream.cuda_stream
     for _ in range(warmup):
         wl.launch(eng, sp)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
+    for _ in range(steps):
         wl.launch(eng, sp)
-        b.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for a, b in ev:
+        a.record(stream)
+        wl.launch(eng, sp)
+        b.record(stream)
+    torch.cuda.synchronize()
     kern = [a.elapsed_time(b) * 1e-3 for a, b in ev]
     if world > 1:
         from ix_amd.shard import max_over_ranks
