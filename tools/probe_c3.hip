@@ -85,6 +85,33 @@ __global__ void __launch_bounds__(256) k_reg2(const uint8_t* base, const uint64_
   }
 }
 
+// reg over spans of CPW consecutive chunks (one contiguous span for packed
+// frames), the waves' spans strided by CPW * nw chunks
+template <int U, int CPW>
+__global__ void __launch_bounds__(256) k_reg3(const uint8_t* base, const uint64_t* off, const uint16_t* len,
+                                              u32x4* out, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nw = gridDim.x * 4, nch = (n + 63) / 64;
+  for (uint32_t c = (blockIdx.x * 4 + (threadIdx.x >> 6)) * CPW; c < nch; c += nw * CPW) {
+    const uint32_t f0 = c * 64, fe = (c + CPW) * 64 < n ? (c + CPW) * 64 : n;
+    const uint64_t b = off[f0] & ~15ull;
+    const uint32_t bytes = (uint32_t)(off[fe - 1] + len[fe - 1] - b);
+    const uint32_t npc = (bytes + 15) / 16;
+    uint32_t a = 0;
+    for (uint32_t q0 = 0; q0 < npc; q0 += 64 * U) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t q = q0 + 64 * u + lane;
+        v[u] = *reinterpret_cast<const u32x4*>(base + b + 16ull * (q < npc ? q : npc - 1));
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) a += hsum(v[u]);
+    }
+    for (uint32_t f = f0 + lane; f < fe; f += 64) out[f] = u32x4{a, f, 0u, 0u};
+  }
+}
+
 constexpr uint32_t kWin = 4096;  // bytes per window (4 glds per lane)
 __global__ void __launch_bounds__(256) k_lds(const uint8_t* base, const uint64_t* off, const uint16_t* len,
                                              u32x4* out, uint32_t n, const uint8_t* zero) {
@@ -151,10 +178,11 @@ __global__ void __launch_bounds__(256) k_lds(const uint8_t* base, const uint64_t
 }
 
 extern "C" const char* p3_name(int w) {
-  static const char* nm[] = {"reg_u4", "reg_u8", "reg_u16", "lds_4k", "reg2_u8", "reg2_u16", "reg2_u24"};
+  static const char* nm[] = {"reg_u4", "reg_u8", "reg_u16", "lds_4k", "reg2_u8", "reg2_u16", "reg2_u24",
+                             "reg3_u16_c4", "reg3_u16_c16", "reg3_u16_c64", "reg3_u8_c4"};
   return nm[w];
 }
-extern "C" int p3_count(void) { return 7; }
+extern "C" int p3_count(void) { return 11; }
 extern "C" int p3_launch(int which, const void* base, const void* off, const void* len, void* out, uint32_t n,
                          const void* zero, uint32_t grid, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -168,6 +196,10 @@ extern "C" int p3_launch(int which, const void* base, const void* off, const voi
   if (which == 4) hipLaunchKernelGGL(k_reg2<8>, dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 5) hipLaunchKernelGGL(k_reg2<16>, dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 6) hipLaunchKernelGGL(k_reg2<24>, dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
+  if (which == 7) hipLaunchKernelGGL((k_reg3<16, 4>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
+  if (which == 8) hipLaunchKernelGGL((k_reg3<16, 16>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
+  if (which == 9) hipLaunchKernelGGL((k_reg3<16, 64>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
+  if (which == 10) hipLaunchKernelGGL((k_reg3<8, 4>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 3) hipLaunchKernelGGL(k_lds, dim3(grid), dim3(256), 0, s, bp, op, lp, o, n, (const uint8_t*)zero);
   return (int)hipGetLastError();
 }
