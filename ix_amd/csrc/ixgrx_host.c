@@ -290,6 +290,8 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		c->variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
 		e = getenv("IXGRX_SHORT_VARIANT");
 		c->variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
+		e = getenv("IXGRX_FLAT");  /* bit 30: the flat long kernel */
+		c->variant |= (e && atoi(e)) ? (1 << 30) : 0;
 	}
 #endif
 	c->ncu = (uint32_t)prop.multiProcessorCount;

@@ -37,7 +37,9 @@ struct ixg_kparams {
 	                          launch; present[0] == epoch iff the sampler ran,
 	                          and then present[3] is the launch's IXG_MODE_*;
 	                          present[4] == epoch iff the parse kernel left
-	                          tails for the tail kernel */
+	                          tails for the tail kernel; present[5] == epoch
+	                          iff the flat kernel walked every chunk
+	                          (IXG_MODE_LONG) and flagged the ones it left */
 	/* the parse / tail split of the long class (with defer): the parse
 	 * kernel leaves each long L4 segment's whole 16-byte pieces past the
 	 * prefix to the tail kernel. tail: 2 x u32x4 per frame index {frame
@@ -69,6 +71,8 @@ struct ixg_kparams {
 	const uint32_t *fdir;
 	uint32_t fdir_mask;
 	uint32_t fdir_fg;      /* IXG_ETH_MAX_TOTAL_FG + cpu_id */
+	uint32_t flat_cap;     /* the flat long kernel: 16-byte pieces of LDS per
+	                          wave (set by ixgrx_launch for that kernel) */
 };
 
 /* the flow-director table's hash (host and device agree on it) */

@@ -1559,7 +1559,10 @@ DEV void general_body(const KParams& p) {
   // a block with no deferred chunk exits before staging the tables (the
   // common case behind the fixed-shape kernel: 64 B frames)
   const uint32_t mode = launch_mode(p);
-  const bool all = CLS == IXG_CLS_SHORT ? mode == IXG_MODE_SHORT : (p.defer == nullptr || mode == IXG_MODE_LONG);
+  // (IXG_MODE_LONG behind the flat kernel: only the chunks it flagged)
+  const bool all = CLS == IXG_CLS_SHORT
+                       ? mode == IXG_MODE_SHORT
+                       : (p.defer == nullptr || (mode == IXG_MODE_LONG && p.present[5] != p.epoch));
   // (p.present is only read when the flags are in use: it is null with
   // p.defer when the general kernel runs alone)
   if (!all) {
@@ -1771,6 +1774,17 @@ constexpr int kSpanWaves = 16;                  // 1024-thread blocks, 1 per CU
 constexpr uint32_t kGldsWait = 0x0F70;          // s_waitcnt vmcnt(0) (gfx9 encoding)
 constexpr uint32_t kLdsWait = 0xC07F;           // s_waitcnt lgkmcnt(0)
 
+// 64-bit wave broadcasts (the builtins return int: each half is taken as
+// uint32_t, or a low word >= 2^31 would sign-extend over the high one)
+DEV uint64_t rfl64(uint64_t x) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+DEV uint64_t rl64(uint64_t x, uint32_t lane) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)x, lane) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), lane) << 32);
+}
+
 // A chunk's span: LDS image of [base, base + 1024 * npc) (npc = 0: not
 // span-contiguous, load per lane)
 struct Span {
@@ -1785,13 +1799,11 @@ DEV Span span_issue(const KParams& p, const GDesc& g, int lane, bool live, lds_u
   Span sp{0, 0};
   if (!live) return sp;
   const uint32_t need = g.L < IXG_SHORT_MAX ? g.L : IXG_SHORT_MAX;
-  const uint64_t base = (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)g.off) |
-                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(g.off >> 32)) << 32);
+  const uint64_t base = rfl64(g.off);
   const uint64_t b16 = base & ~15ull;
   const uint64_t end = g.off + need;
   // the last lane's end bounds the span when the offsets ascend (packed)
-  const uint64_t e63 = (uint64_t)__builtin_amdgcn_readlane((uint32_t)end, 63) |
-                       ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(end >> 32), 63) << 32);
+  const uint64_t e63 = rl64(end, 63);
   const bool ok = g.L == 0u || (g.off >= base && end <= e63 && e63 - b16 <= kSpanMax);
   if (!wave_all(ok)) return sp;
   sp.base = b16;
@@ -1956,6 +1968,296 @@ DEV void short_span_body(const KParams& p) {
   NAME(KParams p) { short_span_body<OFFS, DMX, ##__VA_ARGS__>(p); }
 IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
 IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
+
+// ---- the flat long kernel (A/B builds only) ---------------------------------
+// Measured slower than the general kernel on C3 (1.55-1.58 vs 1.48 ms per
+// launch in same-process A/Bs), kept for reference:
+// IXGRX_FLAT=1 in an A/B build runs it ahead of the general kernel.
+// Long chunks (a frame of IXG_SHORT_MAX bytes or more) whose frames lie in
+// one span of at most p.flat_cap 16-byte pieces (packed batches: C3's IMIX)
+// sum their L4 tails without any per-segment streaming. The wave sweeps the
+// chunk's whole span [sb, se) in rows of 64 consecutive pieces (1 KiB per
+// wave instruction, fully coalesced, every byte fetched once) and stores
+// each piece's one's complement sum in LDS; a lane-blocked scan turns those
+// into exclusive prefix sums P(k) of the span's 32-bit words. One's
+// complement sums are sums mod 2^32 - 1, so a segment's tail [96, seg_end)
+// is P(seg_end) - P(96) (add the complement), each P at a dword boundary
+// inside a piece completed from the lane's own prefix (byte 96) or the piece
+// holding the segment end (one 16-byte load). The parse is the span
+// kernel's (per-lane prefix loads of bytes 12..95, issued right after the
+// first sweep rows). Chunks that are not span-contiguous, or whose span
+// exceeds the LDS, are flagged for the general kernel.
+#ifdef IXGRX_AB
+constexpr int kFlatWaves = 16;  // 1024-thread blocks, one per CU
+constexpr int kFlatU = 2;       // rows per sweep batch (two batches in flight)
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+// one's complement (end-around carry) sum of a piece's four dwords
+DEV uint32_t piece1c(const u32x4& v) {
+  uint32_t a = v.x;
+  asm("v_add_co_u32 %0, vcc, %0, %1\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %2, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %3, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, 0, vcc"
+      : "+v"(a)
+      : "v"(v.y), "v"(v.z), "v"(v.w)
+      : "vcc");
+  return a;
+}
+
+// a sweep batch: rows [r0, r0 + kFlatU) of the span, raw buffer loads
+// through a descriptor bounded to the span (pieces past it read 0 without a
+// memory access); the row offset is a scalar, the lane's a constant
+DEV void flat_issue(__amdgpu_buffer_rsrc_t rs, uint32_t r0, int lane, u32x4 (&v)[kFlatU]) {
+#pragma unroll
+  for (int u = 0; u < kFlatU; u++)
+    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, (int)(1024u * (r0 + (uint32_t)u)), 0);
+}
+
+// (rows past R, the span's last, are not stored: they sum to zero)
+DEV void flat_consume(lds_u32* S, uint32_t r0, uint32_t R, int lane, const u32x4 (&v)[kFlatU]) {
+#pragma unroll
+  for (int u = 0; u < kFlatU; u++)
+    if (r0 + (uint32_t)u < R) S[64u * (r0 + (uint32_t)u) + (uint32_t)lane] = piece1c(v[u]);
+}
+
+DEV void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A chunk's head: its span and, when it fits, its first sweep batch and
+// its prefixes in flight. The walk issues the next chunk's head as soon as
+// the current chunk's sweep has been consumed, so those loads overlap the
+// current chunk's prefix sums and records.
+struct FlatHead {
+  uint32_t chunk;  // kNoChunk: none
+  bool ok;         // fits (else flagged for the general kernel)
+  uint64_t sb;     // span start (16-aligned, relative to p.base)
+  uint32_t npc;    // 16-byte pieces in the span
+  GDesc g;
+  u32x4 A[kFlatU];
+  uint32_t d[kPrefixDw];
+};
+
+template <bool OFFS>
+DEV void flat_head(const KParams& p, uint32_t chunk, const GDesc& g, int lane, FlatHead& h) {
+  h.chunk = chunk;
+  h.g = g;
+  h.ok = false;
+  if (chunk == kNoChunk) return;
+  const uint32_t L = g.L;  // 0 past the batch end
+  // the span: lane 0's frame starts it, the last valid lane's frame ends it,
+  // and every frame lies inside (ascending offsets: packed batches)
+  const uint32_t nv = p.n - chunk * 64u < 64u ? p.n - chunk * 64u : 64u;
+  const uint64_t b0 = rfl64(g.off);
+  const uint64_t end = g.off + L;
+  const uint64_t eL = rl64(end, nv - 1u);
+  const uint64_t sb = b0 & ~15ull;
+  if (!wave_all(L == 0u || (g.off >= b0 && end <= eL)) || eL - sb > 16ull * p.flat_cap) return;
+  const uint32_t npc = (uint32_t)((eL - sb + 15u) >> 4);
+  // R rows of 64 pieces; lane blocks of M pieces (M % 4 == 0, M <= 32)
+  // cover [0, npc] (P(npc) is the total): the blocks starting at or before
+  // npc end before 64 (R + 1), and row R is zeroed
+  if (64u * (((npc + 63u) >> 6) + 1u) > p.flat_cap) return;
+  h.ok = true;
+  h.sb = sb;
+  h.npc = npc;
+  // sweep batch 0, then the prefixes (their lines are among the rows')
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.base + sb), 0, (int)(16u * npc), 0x00020000);
+  flat_issue(rs, 0u, lane, h.A);
+  load_prefix<0, 6>(p.base + g.off, L, reinterpret_cast<const uint8_t*>(p.tab), h.d);
+}
+
+// One chunk whose head h fits; issues the head of chunk `next` (descriptors
+// gn) into h before its prefix sums.
+template <bool OFFS>
+DEV void flat_chunk(const KParams& p, const Tab64& tab, const lds_u32* t6, lds_u32* S, lds_u32* Bs, int lane,
+                    FlatHead& h, uint32_t next, const GDesc& gn) {
+  const uint32_t chunk = h.chunk;
+  const uint32_t i = chunk * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t L = h.g.L;
+  const uint64_t off = h.g.off, sb = h.sb;
+  const uint32_t npc = h.npc;
+  const uint32_t R = (npc + 63u) >> 6;
+  const uint32_t M = (((npc + 64u) >> 6) + 3u) & ~3u;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.base + sb), 0, (int)(16u * npc), 0x00020000);
+  flat_consume(S, 0u, R, lane, h.A);
+
+  // ---- parse ----
+  LaneState st;
+  parse_dispatch(p, tab, h.d, L, valid, st, t6);
+  const bool strm = valid && st.stream;  // segment ending past byte 96
+  const uint32_t r4 = strm ? 0u : l4_residual(st);
+  Rec rok = make_record(p, h.d, L, st, r4);
+  Rec rbad = make_record(p, h.d, L, st, 1u);
+  uint32_t acc32 = fold32(st.l4_acc), ip_res = st.ip_res;
+  const uint32_t kind = (uint32_t)st.l4_kind, seg_end = st.seg_end;
+  // span positions of byte 96 and of the segment end; the dwords of byte
+  // 96's piece before it are the prefix's last (96 - 16 k_x) / 4
+  const uint32_t rel = (uint32_t)(off - sb);
+  uint32_t x = rel + (uint32_t)kStreamBase, y = rel + seg_end;
+  const uint32_t rx = (x & 15u) >> 2;
+  uint32_t px = rx >= 3u ? h.d[21] : 0u;
+  px = add1c(px, rx >= 2u ? h.d[22] : 0u);
+  px = add1c(px, rx >= 1u ? h.d[23] : 0u);
+  const u32x4 ve = load16(strm && (y & 15u) != 0u, p.base + sb + (y & ~15u), p.zero + 16 * lane);
+  asm volatile("" : "+v"(rok.w0), "+v"(rok.w1), "+v"(rok.w2), "+v"(rok.w3));
+  asm volatile("" : "+v"(rbad.w0), "+v"(rbad.w1), "+v"(rbad.w2), "+v"(rbad.w3));
+  asm volatile("" : "+v"(acc32), "+v"(ip_res), "+v"(px), "+v"(x), "+v"(y));
+
+  // ---- the rest of the sweep: two batches in flight, each issued a full
+  // batch ahead of its use ----
+  u32x4 A[kFlatU], B[kFlatU];
+  flat_issue(rs, kFlatU, lane, B);
+  flat_issue(rs, 2u * kFlatU, lane, A);
+#pragma clang loop unroll(disable)
+  for (uint32_t r0 = kFlatU; r0 < R; r0 += 2u * kFlatU) {
+    flat_consume(S, r0, R, lane, B);
+    flat_issue(rs, r0 + 2u * kFlatU, lane, B);
+    flat_consume(S, r0 + kFlatU, R, lane, A);
+    flat_issue(rs, r0 + 3u * kFlatU, lane, A);
+  }
+  S[64u * R + (uint32_t)lane] = 0u;
+  // the next chunk's head: its loads overlap the rest of this chunk
+  flat_head<OFFS>(p, next, gn, lane, h);
+  wave_sync_lds();
+
+  // ---- prefix sums: lane-local exclusive prefixes in place, block bases ----
+  lds_u32* blk = S + (uint32_t)lane * M;
+  const bool inblk = (uint32_t)lane * M <= npc;  // (blocks past npc: never queried, not in S)
+  uint32_t run = 0;
+#pragma clang loop unroll(disable)
+  for (uint32_t j = 0; inblk && j < M; j += 4u) {
+    const u32x4 v = *reinterpret_cast<lds_u32x4*>(blk + j);
+    u32x4 e;
+    e.x = run;
+    run = add1c(run, v.x);
+    e.y = run;
+    run = add1c(run, v.y);
+    e.z = run;
+    run = add1c(run, v.z);
+    e.w = run;
+    run = add1c(run, v.w);
+    *reinterpret_cast<lds_u32x4*>(blk + j) = e;
+  }
+  uint32_t incl = run;
+#pragma unroll
+  for (int k = 1; k < 64; k <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)incl, k);
+    if (lane >= k) incl = add1c(incl, t);
+  }
+  const uint32_t excl = (uint32_t)__shfl_up((int)incl, 1);
+  Bs[lane] = lane == 0 ? 0u : excl;
+  wave_sync_lds();
+
+  // ---- the records ----
+  if (valid) {
+    uint32_t res = r4;
+    if (strm) {
+      // P(k) = Bs[k / M] + S[k]; k / M exactly from a float reciprocal
+      // ((k + 0.5) / M is >= 0.5 / M from an integer, k <= 64 M)
+      const float rcp = __builtin_amdgcn_rcpf((float)M);
+      const uint32_t kx = x >> 4, ky = y >> 4;
+      const uint32_t Px = add1c(add1c(Bs[(uint32_t)(((float)kx + 0.5f) * rcp)], S[kx]), px);
+      const u32x4 vm = mask_piece(ve, (int)(y & 15u));
+      const uint32_t Py = add1c(add1c(Bs[(uint32_t)(((float)ky + 0.5f) * rcp)], S[ky]), piece1c(vm));
+      uint32_t tail = add1c(Py, ~Px);
+      // an ICMP segment whose in-prefix bytes are all zero: the difference
+      // cannot tell an all-zero tail (residual 0xffff) from a non-zero one
+      // that sums to zero; the exact sum, serially (rare)
+      if (kind == 2u && acc32 == 0u) tail = span_sum(p, off, (uint32_t)kStreamBase, seg_end);
+      res = (~fold16(add1c(acc32, tail))) & 0xffffu;
+    }
+    store_record(p, i, (!strm || res == 0u) ? rok : rbad, ip_res, res);
+  }
+  // (every lane has read S and Bs before the next chunk writes them)
+  wave_sync_lds();
+}
+
+template <bool OFFS>
+DEV void flat_body(const KParams& p) {
+  constexpr int W = kFlatWaves;
+  __shared__ uint64_t T[12 * 256];
+  __shared__ uint32_t sh_q[W][64], sh_b[W][64];
+  // dynamic LDS: [the IPv6 tables (IXG_TAB6_WORDS, when p.tab6)] then W
+  // arrays of p.flat_cap piece sums
+  extern __shared__ u32x4 dyn6[];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nw = gridDim.x * W;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t mode = launch_mode(p);
+  // IXG_MODE_LONG: every chunk, each flagged 0 (done here) or IXG_CLS_LONG;
+  // present[5] tells the general kernel to take only the flagged ones
+  const bool all = mode == IXG_MODE_LONG;
+  if (all) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) p.present[5] = p.epoch;
+  } else if (p.present[IXG_CLS_LONG] != p.epoch) {
+    return;  // nothing deferred long
+  }
+  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_LONG; };
+  const uint32_t wv = blockIdx.x * W + wave;
+  bool any = all;
+  for (uint32_t g = 0; !any && wv + 64u * g * nw < nchunks; g++) {
+    const uint32_t ci = wv + (64u * g + (uint32_t)lane) * nw;
+    any = wave_any(ci < nchunks && mine(ci));
+  }
+  if (!__syncthreads_or(any)) return;
+  const uint32_t t6w = p.tab6 ? IXG_TAB6_WORDS : 0u;
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * W)
+      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
+  stage_tables(p, T);
+  const Tab64 tab{T};
+  const lds_u32* t6 = LDS(const lds_u32, dyn6);
+  lds_u32* S = LDS(lds_u32, dyn6) + t6w + (uint32_t)wave * p.flat_cap;
+  lds_u32* Bs = LDS(lds_u32, sh_b[wave]);
+  lds_u32* q = LDS(lds_u32, sh_q[wave]);
+  bool seen = false;
+  // chunks wv, wv + nw, wv + 2 nw, ... (the grid reads one window of the batch)
+  for (uint32_t g0 = 0; wv + 64u * g0 * nw < nchunks; g0++) {
+    const uint32_t ci = wv + (64u * g0 + (uint32_t)lane) * nw;
+    const bool want = ci < nchunks && (all || mine(ci));
+    const uint64_t m = __ballot(want);
+    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
+    const uint32_t nq = (uint32_t)__popcll(m);
+    __builtin_amdgcn_wave_barrier();
+    if (nq == 0) continue;
+    GDesc D0, D1;
+    gen_desc<OFFS>(p, q[0], lane, D0);
+    const uint32_t c1 = nq > 1 ? q[1] : kNoChunk;
+    gen_desc<OFFS>(p, c1, lane, D1);
+    FlatHead H;
+    flat_head<OFFS>(p, q[0], D0, lane, H);
+    for (uint32_t j = 0; j < nq; j++) {
+      const uint32_t c = H.chunk, cn = j + 1 < nq ? q[j + 1] : kNoChunk;
+      GDesc D2;
+      gen_desc<OFFS>(p, j + 2 < nq ? q[j + 2] : kNoChunk, lane, D2);
+      const bool done = H.ok;
+      if (lane == 0) p.defer[c] = done ? (uint8_t)0 : (uint8_t)IXG_CLS_LONG;
+      seen |= !done;
+      if (done)
+        flat_chunk<OFFS>(p, tab, t6, S, Bs, lane, H, cn, D1);
+      else
+        flat_head<OFFS>(p, cn, D1, lane, H);
+      D1 = D2;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
+}
+
+extern "C" __global__ void __launch_bounds__(64 * kFlatWaves) __attribute__((amdgpu_waves_per_eu(4)))
+ixg_rx_flat_s(KParams p) { flat_body<false>(p); }
+extern "C" __global__ void __launch_bounds__(64 * kFlatWaves) __attribute__((amdgpu_waves_per_eu(4)))
+ixg_rx_flat_o(KParams p) { flat_body<true>(p); }
+#endif  // IXGRX_AB (flat kernel)
+
 #ifdef IXGRX_AB
 IXG_SPAN_KERNEL(ixg_rx_short_spnt_s, false, false, 0, false)
 IXG_SPAN_KERNEL(ixg_rx_short_spnt_o, true, false, 0, false)
@@ -2456,6 +2758,13 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
 }
 
 typedef void (*kern_fn)(KParams);
+#ifdef IXGRX_AB
+// LDS per workgroup (gfx950); the flat kernel's dynamic part is this less
+// its static arrays (hash tables, per-wave chunk queues and block bases)
+constexpr size_t kLdsMax = 160u * 1024u;
+// variant bit 30: the flat long kernel (A/B builds)
+constexpr int kFlatOn = 1 << 30;
+#endif
 // [variant][layout: 0 = stride, 1 = offsets]; the product library has only
 // variant 0 (the default kernels)
 static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o}
@@ -2602,6 +2911,34 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     hipLaunchKernelGGL(ixg_rx_tail, dim3(grid_for(ixg_rx_tail, group_blocks, ncu)), dim3(kBlock), 0,
                        (hipStream_t)stream, p);
     return (int)hipGetLastError();
+  }
+#endif
+  // A/B builds, IXGRX_FLAT=1: the flat long kernel (not with the fused
+  // demux) takes the long chunks whose span fits its LDS, the general kernel
+  // the rest
+#ifdef IXGRX_AB
+  if (p.defer && !p.dmx && gv == 0 && (variant & kFlatOn)) {
+    static std::once_flag once;
+    static size_t dyn_max = 0;
+    std::call_once(once, [] {
+      size_t st = 0;
+      for (kern_fn k : {ixg_rx_flat_s, ixg_rx_flat_o}) {
+        hipFuncAttributes a;
+        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k)) == hipSuccess && a.sharedSizeBytes > st)
+          st = a.sharedSizeBytes;
+      }
+      dyn_max = kLdsMax - (st ? st : 40u * 1024u);
+      for (kern_fn k : {ixg_rx_flat_s, ixg_rx_flat_o})
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)dyn_max);
+    });
+    KParams pf = p;
+    pf.flat_cap = (uint32_t)((dyn_max - sh6) / (4u * kFlatWaves)) & ~63u;
+    const size_t dyn = sh6 + (size_t)pf.flat_cap * 4u * kFlatWaves;
+    const kern_fn kfl = lay ? ixg_rx_flat_o : ixg_rx_flat_s;
+    const uint64_t want = ((nchunks + 63u) / 64u + kFlatWaves - 1) / kFlatWaves;
+    hipLaunchKernelGGL(kfl, dim3(grid_for(kfl, want, ncu, dyn, 64 * kFlatWaves)), dim3(64 * kFlatWaves), dyn,
+                       (hipStream_t)stream, pf);
   }
 #endif
   const kern_fn kg = k_gen[gv][lay];

@@ -170,6 +170,40 @@ def test_device_path_torch_stream(engines):
     assert (cs.cpu().numpy().view(np.uint32) == ec).all()
 
 
+@pytest.mark.parametrize("kind", ["mixed", "imix"])
+def test_offsets_past_2_and_4_gib(kind, engines):
+    """u64 offsets with bit 31 and bit 32 set (batches over 2 GiB, like C3's
+    6 GB and C4's): frames placed across the 2 GiB and 4 GiB marks of one
+    4.3 GB buffer. Covers the kernels' 64-bit wave broadcasts of frame
+    offsets (the span kernel's staging decision read a low word >= 2^31 as
+    negative and sign-extended it; those chunks silently took per-lane
+    loads)."""
+    import torch
+    tr = traces.make_trace(kind, 20000, seed=77, bad_ip=0.01, bad_l4=0.01)
+    er, ec = oracle.rx_trace(tr, KEY, threads=8, hash_mode=oracle.HASH_TABLE)
+    dev = torch.device("cuda:0")
+    span = int(tr.off[-1]) + int(tr.len[-1])
+    src = torch.from_numpy(np.ascontiguousarray(tr.blob[:span])).to(dev)
+    buf = torch.zeros((1 << 32) + span + 4096, dtype=torch.uint8, device=dev)
+    lens = torch.from_numpy(tr.len.astype(np.int16)).to(dev)
+    out = torch.empty((tr.n, 16), dtype=torch.uint8, device=dev)
+    cs = torch.empty(tr.n, dtype=torch.int32, device=dev)
+    try:
+        for base in ((1 << 31) - span // 2, (1 << 32) - span // 3):
+            base &= ~15
+            buf[base:base + span] = src
+            off = torch.from_numpy(tr.offsets().astype(np.int64) + base).to(dev)
+            out.zero_()
+            engines().batch_dev(buf.data_ptr(), off.data_ptr(), lens.data_ptr(), 0, tr.n, out.data_ptr(),
+                                cs.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            _diff(out.cpu().numpy(), er, f"{kind} at base {base:#x}")
+            assert (cs.cpu().numpy().view(np.uint32) == ec).all()
+    finally:
+        del buf
+        torch.cuda.empty_cache()
+
+
 def test_full_size_tcp64_tiled(engines):
     """C2 at full size (16M frames): records must be the pool's records tiled."""
     import torch
