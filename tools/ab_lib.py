@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=8)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--general", action="store_true", help="general kernel alone (ixg_rx_set_split) for every build")
+    ap.add_argument("--splits", default=None, help="comma list of ixg_rx_set_split modes to time per build "
+                                                     "(auto, fast, short, long, general)")
     args = ap.parse_args()
     import torch
     import bench
@@ -31,10 +33,12 @@ def main():
     dev = torch.device("cuda:0")
     wl = bench.Workload(args.workload, seed=0x1B0002, dev=dev)
     engs = {}
+    splits = args.splits.split(",") if args.splits else ["general" if args.general else "auto"]
     for path in args.libs.split(","):
-        engs[os.path.basename(path)] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags),
-                                                      lib_path=os.path.join(ROOT, path),
-                                                      split="general" if args.general else "auto")
+        for sp in splits:
+            name = os.path.basename(path) + ("" if len(splits) == 1 else ":" + sp)
+            engs[name] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags),
+                                        lib_path=os.path.join(ROOT, path), split=sp)
     s = torch.cuda.current_stream()
     # parity: every build's records equal the first build's, and each tiled
     # batch is self-consistent (the oracle checks the first build in tests/)
