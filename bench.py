@@ -742,6 +742,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--secondary", default="c4", help="second workload line ('' to skip)")
+    ap.add_argument("--extra", default="c3,c5", help="further workload lines (BASELINE configs[2] and [4]; "
+                                                      "'' to skip)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-copy", action="store_true")
@@ -853,6 +855,30 @@ def main():
                             "alg_bytes_per_pkt": round(wl2.bytes_per_pkt, 1),
                             "parity": "tiled-consistent" if tiled2 else "MISMATCH"}
         wl = wl2
+    # the other configs as lines of their own: C3 (IMIX) and C5 (IPv4
+    # options + IPv6), weak-scaled like the primary at N > 1; 40 warm-up
+    # launches (C5's first ~35 launches after its batch is built run slower,
+    # DESIGN.md 4.8)
+    extras = [w for w in (args.extra.split(",") if args.extra else [])
+              if w and w not in (args.workload, args.secondary)]
+    for k, name in enumerate(extras):
+        del wl
+        wl = None
+        torch.cuda.empty_cache()
+        wle = Workload(name, seed=0x1B0000 + 6 + k + 97 * rank, dev=dev)
+        ke = max(20, args.steps)
+        ele, kea, kem = time_steps(wle, engine(wle.flags), ke, max(40, args.warmup), dist, world)
+        te, fe = wle.snapshot()
+        checks.append(("rx", wle.name, wle.pool, wle.flags, fe, te))
+        me = wle.n * ke * world / ele / 1e6
+        tr_e, _ = load_traffic(name)
+        res.setdefault("lines", {})[name] = {
+            "workload": wle.desc, "mpps": round(me, 2), "gbps_algorithmic": round(me * wle.bytes_per_pkt / 1e3, 1),
+            "roofline_frac": round(wle.bytes_per_pkt * wle.n / kea / 1e9 / PEAK_HBM_GBPS, 4),
+            "kernel_ms_avg": round(kea * 1e3, 4), "kernel_ms_min": round(kem * 1e3, 4),
+            "alg_bytes_per_pkt": round(wle.bytes_per_pkt, 1), "traffic": tr_e, "kernel": kernels(wle),
+            "parity": "tiled-consistent" if te else "MISMATCH"}
+        wl = wle
     if not args.no_strong and args.workload == "c2":
         del wl
         wl = None
@@ -909,6 +935,8 @@ def main():
         res["parity"] = par[wl_name]
         if "secondary" in res:
             res["secondary"]["parity"] = par[args.secondary]
+        for name in res.get("lines", {}):
+            res["lines"][name]["parity"] = par[name]
         if "c4_strong" in res:
             res["c4_strong"]["parity"] = par["c4_strong"]
         if "demux" in res:
