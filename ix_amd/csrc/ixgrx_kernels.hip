@@ -399,10 +399,25 @@ DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixD
 
   // ---- [NIC] RSS Toeplitz + tcp_to_idx via the byte tables ----
   const bool rss4 = hdr_ok && !frag && (proto == 6 || proto == 17) && (uint32_t)(l4 + 4) <= L;
+  // The 12 lookups serve both families: an IPv4 lane looks up its tuple
+  // (src, dst, ports), an IPv6 lane the first 12 bytes of its 36-byte tuple
+  // (frame bytes 22..33: the same key offsets, so the same tables' Toeplitz
+  // words; its bucket is never used). A mixed wave then runs 12 + 24
+  // lookups instead of 12 + 36.
   uint64_t hx = 0;
-  if (SHAPE != kShapeV6) {  // (IPv6 lanes use neither the v4 RSS nor the bucket)
+  {
     const uint32_t t4 = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+    const uint32_t a6 = (d[5] >> 16) | (d[6] << 16);  // bytes 22..25
     uint32_t sb = src, db = dst, pb = t4;
+    if (SHAPE == kShapeV6) {
+      sb = a6; db = src; pb = dst;
+    } else if (SHAPE == kShapeAny) {
+      uint32_t m6 = 0u - (uint32_t)v6;
+      asm volatile("" : "+v"(m6));
+      sb = bsel(m6, a6, src);
+      db = bsel(m6, src, dst);
+      pb = bsel(m6, dst, t4);
+    }
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       hx ^= T.look(k, (sb >> (8 * k)) & 0xffu);
@@ -420,11 +435,11 @@ DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixD
   // offsets (their low words), positions 12..35 come from the IPv6 tables
   // staged in LDS by the general kernels (IXG_TAB6_WORDS)
   if (SHAPE != kShapeFixed && SHAPE != kShapeV4 && v6 && L >= 58 && ver == 6 && (s.proto == 6 || s.proto == 17)) {
-    uint32_t h = 0;
+    uint32_t h = (uint32_t)hx;  // tuple bytes 0..11, above
 #pragma unroll
-    for (int k = 0; k < 36; k++) {
+    for (int k = 12; k < 36; k++) {
       const uint32_t b = byte_at(d, k < 32 ? 22 + k : 54 + (k - 32));
-      h ^= k < 12 ? (uint32_t)T.look(k, b) : T6[((k - 12) << 8) | b];
+      h ^= T6[((k - 12) << 8) | b];
     }
     s.rss = h;
     s.flags |= IXG_RF_RSS;
