@@ -8,7 +8,7 @@ mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for W in "$@"; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/$W" -o kt -- python3 bench.py \
-    --workload "$W" --secondary "" --no-cpu --no-copy --no-demux --no-tx --no-bad --no-strong --steps 10 --warmup 2 \
+    --workload "$W" --secondary "" --extra "" --no-cpu --no-copy --no-demux --no-tx --no-bad --no-strong --steps 10 --warmup 2 \
     > "$O/$W.json" 2> "$O/$W.log" || { echo "kt $W failed"; tail -20 "$O/$W.log"; exit 1; }
   rm -f "$O/$W"/*kernel_trace.csv
   python3 - "$O/$W/kt_kernel_stats.csv" "$W" <<'PY'

@@ -19,7 +19,7 @@ SPECS=""
 for W in c2 c4 c3 c5 c5r; do
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_${W}_$C" -o p -- python3 bench.py --workload $W \
-      --secondary '' --no-cpu --no-copy --no-demux --no-tx --no-bad --no-strong --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
+      --secondary '' --extra '' --no-cpu --no-copy --no-demux --no-tx --no-bad --no-strong --steps 5 --warmup 1 > "$O/pmc_${W}_$C.json" 2> "$O/pmc_${W}_$C.log" \
       || { echo "pmc $W $C failed"; tail -20 "$O/pmc_${W}_$C.log"; exit 1; }
     find "$O/pmc_${W}_$C" -type f -exec ls -la {} \;
     [ -n "$(find "$O/pmc_${W}_$C" -name '*counter_collection.csv')" ] || { echo "no csv: $W $C"; tail -30 "$O/pmc_${W}_$C.log"; find "$O" -size +1M -delete; exit 1; }
