@@ -38,10 +38,10 @@ def kernels(wl) -> str:
     when its class has nothing deferred), or behind the coalesced kernel one
     general kernel taking both classes (ixg_rx_any_s)."""
     if wl.off is not None:
-        return "ixg_rx_sample + ixg_rx_fast_o + ixg_rx_short_sp_o + ixg_rx_general_o"
+        return "ixg_rx_short_sp_o (samples the launch mode itself) + ixg_rx_general_o"
     if wl.stride <= 64:
         return "ixg_rx_fastc_s (deferred chunks finished in the same dispatch)"
-    return "ixg_rx_sample + ixg_rx_fast_s + ixg_rx_short_sp_s + ixg_rx_general_s"
+    return "ixg_rx_short_sp_s (samples the launch mode itself) + ixg_rx_general_s"
 
 
 WORKLOADS = {

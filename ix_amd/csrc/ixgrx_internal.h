@@ -34,7 +34,8 @@ struct ixg_kparams {
 	                          kernel does everything */
 	uint32_t *present;     /* [IXG_PRESENT_WORDS]: present[k] == epoch (k = 1, 2)
 	                          iff some chunk of class k was deferred in this
-	                          launch; present[0] == epoch iff the sampler ran,
+	                          launch; present[0] == epoch iff the sampler (or
+	                          the self-sampling short kernel) ran,
 	                          and then present[3] is the launch's IXG_MODE_*;
 	                          present[4] == epoch iff the parse kernel left
 	                          tails for the tail kernel; present[5] == epoch
@@ -73,6 +74,9 @@ struct ixg_kparams {
 	uint32_t fdir_fg;      /* IXG_ETH_MAX_TOTAL_FG + cpu_id */
 	uint32_t flat_cap;     /* the flat long kernel: 16-byte pieces of LDS per
 	                          wave (set by ixgrx_launch for that kernel) */
+	uint32_t self_sample;  /* set by ixgrx_launch for the span-staged short
+	                          kernel when it runs first: it samples the
+	                          launch's mode itself and publishes it */
 };
 
 /* the flow-director table's hash (host and device agree on it) */

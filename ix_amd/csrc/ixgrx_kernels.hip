@@ -1203,6 +1203,58 @@ DEV uint32_t launch_mode(const KParams& p) {
   return (p.defer && p.present[0] == p.epoch) ? p.present[3] : IXG_MODE_FAST;
 }
 
+// The launch's IXG_MODE_* from the lengths of up to 64 evenly spread chunks,
+// for a block of W waves (block-uniform; every thread returns it). Every
+// length load is issued before the first vote: one round trip, not one per
+// sample (the sampling is on every launch's critical path).
+template <int W>
+DEV uint32_t sample_mode(const KParams& p, uint32_t (*cnt)[2]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t ns = nchunks < 64u ? nchunks : 64u;
+  constexpr int kPer = 64 / W;
+  uint32_t L[kPer];
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const uint32_t k = (uint32_t)wave + (uint32_t)(W * j);
+    const uint32_t c = ns ? k * nchunks / ns : 0u;  // k * nchunks < 64 * 2^26
+    const uint32_t i = c * 64u + (uint32_t)lane;
+    const bool ok = k < ns && i < p.n;
+    const uint32_t v = p.len[ok ? i : 0u];
+    L[j] = ok ? v : 0u;
+  }
+  uint32_t nf = 0, nsh = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    if ((uint32_t)wave + (uint32_t)(W * j) >= ns) break;
+    nf += wave_all(L[j] <= 64u) ? 1u : 0u;
+    nsh += wave_all(L[j] < IXG_SHORT_MAX) ? 1u : 0u;
+  }
+  if (lane == 0) {
+    cnt[wave][0] = nf;
+    cnt[wave][1] = nsh;
+  }
+  __syncthreads();
+  uint32_t f = 0, sh = 0;
+#pragma unroll
+  for (int w = 0; w < W; w++) {
+    f += cnt[w][0];
+    sh += cnt[w][1];
+  }
+  uint32_t mode = 2 * f >= ns ? IXG_MODE_FAST : (2 * sh >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
+  if (p.force_mode != IXG_MODE_AUTO) mode = p.force_mode;
+  return mode;
+}
+
+// publish a launch's mode for the kernels after this one (launch_mode)
+DEV void publish_mode(const KParams& p, uint32_t mode) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    p.present[3] = mode;
+    p.present[0] = p.epoch;
+  }
+}
+
+
 // returns 1 << class for a deferred chunk, 0 when done here
 DEV uint32_t fast_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, uint32_t L,
                         const Prefix& x) {
@@ -1868,9 +1920,24 @@ DEV void short_span_body(const KParams& p) {
   const uint32_t nw = gridDim.x * W;
   const uint32_t nchunks = (p.n + 63u) >> 6;
   const uint32_t ngroups = (nchunks + 63u) >> 6;
-  const uint32_t mode = launch_mode(p);
+  // p.self_sample (the default plan for offset and wide-stride batches):
+  // no sampler or fixed-shape kernel ran before this one; every block
+  // samples the launch's mode itself (the same lengths: L2 hits after the
+  // first blocks), block 0 publishes it for the long kernel, and FAST counts
+  // as SHORT (this kernel takes fixed-shape chunks at the fixed-shape
+  // kernel's speed: C2's frames in the offset layout within 1.2 %). Two
+  // dispatches fewer per launch: ~10 us (C5 -2 %).
+  __shared__ uint32_t cnt[W][2];
+  uint32_t mode;
+  if (p.self_sample) {
+    mode = sample_mode<W>(p, cnt);
+    if (mode == IXG_MODE_FAST) mode = IXG_MODE_SHORT;
+    publish_mode(p, mode);
+  } else {
+    mode = launch_mode(p);
+  }
   const bool all = mode == IXG_MODE_SHORT;
-  if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
+  if (!all && (mode == IXG_MODE_LONG || p.present[IXG_CLS_SHORT] != p.epoch)) return;  // nothing deferred short
   auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
   bool any = all;
   {
@@ -2727,52 +2794,12 @@ IXG_GEN_KERNEL(ixg_rx_general_w3nb_s, false, IXG_CLS_LONG, 3, false, 1, false, f
 IXG_GEN_KERNEL(ixg_rx_general_w3nb_o, true, IXG_CLS_LONG, 3, false, 1, false, false)
 #endif
 
-// The sampler: one block reads the lengths of up to 64 evenly spread chunks
-// and picks the launch's IXG_MODE_* (ixgrx_internal.h): FAST when at least
-// half of them could be fixed-shape by length (every frame <= 64 B), else
-// SHORT when at least half are short, else LONG.
+// The sampler: one block picks the launch's IXG_MODE_*: FAST when at least
+// half of the sampled chunks could be fixed-shape by length (every frame <=
+// 64 B), else SHORT when at least half are short, else LONG.
 extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
   __shared__ uint32_t cnt[kWaves][2];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t ns = nchunks < 64u ? nchunks : 64u;
-  // every length load issued before the first vote (one round trip, not one
-  // per sample: the sampler is on every launch's critical path)
-  constexpr int kPer = 64 / kWaves;
-  uint32_t L[kPer];
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    const uint32_t k = (uint32_t)wave + (uint32_t)(kWaves * j);
-    const uint32_t c = ns ? k * nchunks / ns : 0u;  // k * nchunks < 64 * 2^26
-    const uint32_t i = c * 64u + (uint32_t)lane;
-    const bool ok = k < ns && i < p.n;
-    const uint32_t v = p.len[ok ? i : 0u];
-    L[j] = ok ? v : 0u;
-  }
-  uint32_t nf = 0, nsh = 0;
-#pragma unroll
-  for (int j = 0; j < kPer; j++) {
-    if ((uint32_t)wave + (uint32_t)(kWaves * j) >= ns) break;
-    nf += wave_all(L[j] <= 64u) ? 1u : 0u;
-    nsh += wave_all(L[j] < IXG_SHORT_MAX) ? 1u : 0u;
-  }
-  if (lane == 0) {
-    cnt[wave][0] = nf;
-    cnt[wave][1] = nsh;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t f = 0, sh = 0;
-#pragma unroll
-    for (int w = 0; w < kWaves; w++) {
-      f += cnt[w][0];
-      sh += cnt[w][1];
-    }
-    uint32_t mode = 2 * f >= ns ? IXG_MODE_FAST : (2 * sh >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
-    if (p.force_mode != IXG_MODE_AUTO) mode = p.force_mode;
-    p.present[3] = mode;
-    p.present[0] = p.epoch;
-  }
+  publish_mode(p, sample_mode<kWaves>(p, cnt));
 }
 
 typedef void (*kern_fn)(KParams);
@@ -2881,7 +2908,12 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&
                       (reinterpret_cast<uintptr_t>(p.base) & 15u) == 0u;
   const size_t sh6 = p.tab6 ? IXG_TAB6_WORDS * sizeof(uint32_t) : 0u;
-  if (p.defer) {
+  // offset and wide-stride batches in the default split: the span-staged
+  // short kernel runs first and samples the mode itself (no sampler, no
+  // fixed-shape kernel dispatch); forced splits, the fused demux and the A/B
+  // variants keep the sampler + fixed-shape kernel plan
+  const bool self = p.defer && !coal && fv == 0 && sv == 0 && !p.dmx && p.force_mode == IXG_MODE_AUTO;
+  if (p.defer && !self) {
     kern_fn kf = nullptr;
     const bool forced = p.force_mode != IXG_MODE_AUTO;
     if (fv == 0 && coal) {
@@ -2917,8 +2949,10 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     // one block per 64 chunks per wave
     const uint64_t ngroups = (nchunks + 63u) / 64u, bw = (uint64_t)ks.block / 64u;
     const uint64_t want = (ngroups + bw - 1) / bw;
+    KParams ps = p;
+    ps.self_sample = self ? 1u : 0u;
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
-                       (hipStream_t)stream, p);
+                       (hipStream_t)stream, ps);
   }
 #ifdef IXGRX_AB
   // the parse / tail split: the parse kernel, then the tail kernel over the
