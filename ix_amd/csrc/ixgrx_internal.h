@@ -40,7 +40,9 @@ struct ixg_kparams {
 	                          present[4] == epoch iff the parse kernel left
 	                          tails for the tail kernel; present[5] == epoch
 	                          iff the flat kernel walked every chunk
-	                          (IXG_MODE_LONG) and flagged the ones it left */
+	                          (IXG_MODE_LONG) and flagged the ones it left;
+	                          present[6] != 0: most sampled chunks are big
+	                          (the long kernel walks its chunks strided) */
 	/* the parse / tail split of the long class (with defer): the parse
 	 * kernel leaves each long L4 segment's whole 16-byte pieces past the
 	 * prefix to the tail kernel. tail: 2 x u32x4 per frame index {frame

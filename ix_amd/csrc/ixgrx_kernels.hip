@@ -1208,7 +1208,7 @@ DEV uint32_t launch_mode(const KParams& p) {
 // length load is issued before the first vote: one round trip, not one per
 // sample (the sampling is on every launch's critical path).
 template <int W>
-DEV uint32_t sample_mode(const KParams& p, uint32_t (*cnt)[2]) {
+DEV uint32_t sample_mode(const KParams& p, uint32_t (*cnt)[3], uint32_t& big) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nchunks = (p.n + 63u) >> 6;
   const uint32_t ns = nchunks < 64u ? nchunks : 64u;
@@ -1223,36 +1223,45 @@ DEV uint32_t sample_mode(const KParams& p, uint32_t (*cnt)[2]) {
     const uint32_t v = p.len[ok ? i : 0u];
     L[j] = ok ? v : 0u;
   }
-  uint32_t nf = 0, nsh = 0;
+  uint32_t nf = 0, nsh = 0, nb = 0;
 #pragma unroll
   for (int j = 0; j < kPer; j++) {
     if ((uint32_t)wave + (uint32_t)(W * j) >= ns) break;
     nf += wave_all(L[j] <= 64u) ? 1u : 0u;
     nsh += wave_all(L[j] < IXG_SHORT_MAX) ? 1u : 0u;
+    nb += wave_all(L[j] >= 256u || L[j] == 0u) ? 1u : 0u;  // (kBigMin)
   }
   if (lane == 0) {
     cnt[wave][0] = nf;
     cnt[wave][1] = nsh;
+    cnt[wave][2] = nb;
   }
   __syncthreads();
-  uint32_t f = 0, sh = 0;
+  uint32_t f = 0, sh = 0, b = 0;
 #pragma unroll
   for (int w = 0; w < W; w++) {
     f += cnt[w][0];
     sh += cnt[w][1];
+    b += cnt[w][2];
   }
   uint32_t mode = 2 * f >= ns ? IXG_MODE_FAST : (2 * sh >= ns ? IXG_MODE_SHORT : IXG_MODE_LONG);
   if (p.force_mode != IXG_MODE_AUTO) mode = p.force_mode;
+  big = 2 * b >= ns ? 1u : 0u;
   return mode;
 }
 
-// publish a launch's mode for the kernels after this one (launch_mode)
-DEV void publish_mode(const KParams& p, uint32_t mode) {
+// publish a launch's mode for the kernels after this one (launch_mode), and
+// whether most sampled chunks are big (every frame >= 256 B: the long
+// kernel then walks its chunks strided, launch_big)
+DEV void publish_mode(const KParams& p, uint32_t mode, uint32_t big) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     p.present[3] = mode;
+    p.present[6] = big;
     p.present[0] = p.epoch;
   }
 }
+
+DEV bool launch_big(const KParams& p) { return p.defer && p.present[0] == p.epoch && p.present[6] != 0u; }
 
 
 // returns 1 << class for a deferred chunk, 0 when done here
@@ -1661,13 +1670,24 @@ DEV void general_body(const KParams& p) {
   bool seen = false;
   // groups g0, g0+nw, ... of this wave, kQGroups at a time: their deferred
   // chunk ids go to an LDS list, which the pipeline then walks
-  for (uint32_t g0 = blockIdx.x * kWaves + wave; g0 < ngroups; g0 += kQGroups * nw) {
+  // Chunk order: wave w takes groups of 64 consecutive chunks (w, w + nw,
+  // ...), or, when most sampled chunks are big (1500-B frames), chunks w,
+  // w + nw, w + 2 nw, ... so the grid reads one window of the batch at a
+  // time: C4 -3.8 %, C3 +7.8 % in same-process A/Bs of the two orders
+  const uint32_t wv0 = blockIdx.x * kWaves + wave;
+  const bool strided = CLS == IXG_CLS_LONG && launch_big(p);
+  for (uint32_t it = 0; (uint64_t)wv0 + (strided ? 64ull * nw * kQGroups * it : (uint64_t)kQGroups * nw * it) <
+                        (strided ? (uint64_t)nchunks : (uint64_t)ngroups);
+       it++) {
+    const uint32_t g0 = wv0 + kQGroups * nw * it;
     uint32_t nq = 0;
 #pragma unroll
     for (int k = 0; k < kQGroups; k++) {
       const uint32_t g = g0 + (uint32_t)k * nw;
-      const uint32_t ci = g * 64u + (uint32_t)lane;
-      const bool want = g < ngroups && ci < nchunks && (all || mine(ci));
+      const uint64_t c64 = strided ? (uint64_t)wv0 + (uint64_t)nw * ((uint32_t)lane + 64ull * (it * kQGroups + (uint32_t)k))
+                                   : (uint64_t)g * 64u + (uint32_t)lane;
+      const uint32_t ci = c64 < nchunks ? (uint32_t)c64 : 0u;
+      const bool want = (strided || g < ngroups) && c64 < nchunks && (all || mine(ci));
       const uint64_t m = __ballot(want);
       if (want) q[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
       nq += (uint32_t)__popcll(m);
@@ -1927,12 +1947,13 @@ DEV void short_span_body(const KParams& p) {
   // as SHORT (this kernel takes fixed-shape chunks at the fixed-shape
   // kernel's speed: C2's frames in the offset layout within 1.2 %). Two
   // dispatches fewer per launch: ~10 us (C5 -2 %).
-  __shared__ uint32_t cnt[W][2];
+  __shared__ uint32_t cnt[W][3];
   uint32_t mode;
   if (p.self_sample) {
-    mode = sample_mode<W>(p, cnt);
+    uint32_t big;
+    mode = sample_mode<W>(p, cnt, big);
     if (mode == IXG_MODE_FAST) mode = IXG_MODE_SHORT;
-    publish_mode(p, mode);
+    publish_mode(p, mode, big);
   } else {
     mode = launch_mode(p);
   }
@@ -2798,8 +2819,10 @@ IXG_GEN_KERNEL(ixg_rx_general_w3nb_o, true, IXG_CLS_LONG, 3, false, 1, false, fa
 // half of the sampled chunks could be fixed-shape by length (every frame <=
 // 64 B), else SHORT when at least half are short, else LONG.
 extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
-  __shared__ uint32_t cnt[kWaves][2];
-  publish_mode(p, sample_mode<kWaves>(p, cnt));
+  __shared__ uint32_t cnt[kWaves][3];
+  uint32_t big;
+  const uint32_t mode = sample_mode<kWaves>(p, cnt, big);
+  publish_mode(p, mode, big);
 }
 
 typedef void (*kern_fn)(KParams);
