@@ -824,6 +824,9 @@ struct GPre {
 };
 
 constexpr uint32_t kNoChunk = 0xffffffffu;
+// the long kernel's chunk order: runs of kRun consecutive chunks per wave,
+// kRunBig when the sample is mostly big chunks (general_body)
+constexpr uint64_t kRun = 64, kRunBig = 1;
 // big chunks: every frame at least this long (or past the batch end)
 constexpr uint32_t kBigMin = 256;
 
@@ -1674,20 +1677,18 @@ DEV void general_body(const KParams& p) {
   // ...), or, when most sampled chunks are big (1500-B frames), chunks w,
   // w + nw, w + 2 nw, ... so the grid reads one window of the batch at a
   // time: C4 -3.8 %, C3 +7.8 % in same-process A/Bs of the two orders
+  // (in general: the wave's j-th chunk is ((j / G) nw + w) G + j % G, runs
+  // of G consecutive chunks dealt out round-robin; G = 64 or 1)
   const uint32_t wv0 = blockIdx.x * kWaves + wave;
-  const bool strided = CLS == IXG_CLS_LONG && launch_big(p);
-  for (uint32_t it = 0; (uint64_t)wv0 + (strided ? 64ull * nw * kQGroups * it : (uint64_t)kQGroups * nw * it) <
-                        (strided ? (uint64_t)nchunks : (uint64_t)ngroups);
-       it++) {
-    const uint32_t g0 = wv0 + kQGroups * nw * it;
+  const uint64_t G = CLS == IXG_CLS_LONG && launch_big(p) ? kRunBig : kRun;
+  for (uint32_t it = 0; ((uint64_t)64u * kQGroups * it / G * nw + wv0) * G < nchunks; it++) {
     uint32_t nq = 0;
 #pragma unroll
     for (int k = 0; k < kQGroups; k++) {
-      const uint32_t g = g0 + (uint32_t)k * nw;
-      const uint64_t c64 = strided ? (uint64_t)wv0 + (uint64_t)nw * ((uint32_t)lane + 64ull * (it * kQGroups + (uint32_t)k))
-                                   : (uint64_t)g * 64u + (uint32_t)lane;
+      const uint64_t j = (uint32_t)lane + 64ull * (it * kQGroups + (uint32_t)k);
+      const uint64_t c64 = (j / G * nw + wv0) * G + j % G;
       const uint32_t ci = c64 < nchunks ? (uint32_t)c64 : 0u;
-      const bool want = (strided || g < ngroups) && c64 < nchunks && (all || mine(ci));
+      const bool want = c64 < nchunks && (all || mine(ci));
       const uint64_t m = __ballot(want);
       if (want) q[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
       nq += (uint32_t)__popcll(m);
