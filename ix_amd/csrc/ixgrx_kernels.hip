@@ -827,6 +827,9 @@ constexpr uint32_t kNoChunk = 0xffffffffu;
 // the long kernel's chunk order: runs of kRun consecutive chunks per wave,
 // kRunBig when the sample is mostly big chunks (general_body)
 constexpr uint64_t kRun = 64, kRunBig = 1;
+// the coalesced fixed-shape kernel's (fastc_loop)
+constexpr uint32_t kRunC = 2;
+static_assert(64 % kRunC == 0, "whole runs within a wave's 64 drained chunks");
 // big chunks: every frame at least this long (or past the batch end)
 constexpr uint32_t kBigMin = 256;
 
@@ -1477,9 +1480,15 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  // the wave's k-th chunk: runs of kRunC consecutive chunks dealt out
+  // round-robin (kRunC = 1: grid-stride, the grid reads one window)
+  const uint32_t w0 = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  auto chunk_of = [&](uint32_t k) -> uint32_t {
+    const uint64_t c64 = ((uint64_t)(k / kRunC) * nw + w0) * kRunC + k % kRunC;
+    return c64 < nchunks ? (uint32_t)c64 : nchunks;
+  };
+  uint32_t c = chunk_of(0);
   if (c >= nchunks) return;
-  const uint32_t c_first = c;
   uint64_t dmask = 0;  // bit k: the wave's k-th chunk was not fixed-shape
   uint32_t kth = 0;
   // readable bytes: up to IXG_TAIL_PAD past the last frame's end
@@ -1491,7 +1500,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   if (DMX) pend.i = kNoDmx;
   fastc_issue(p, c, nchunks, lim, lane, cur, Lc);
   for (;;) {
-    const uint32_t cn = c + nw;
+    const uint32_t cn = chunk_of(kth + 1);
     u32x4 nxt[4];
     uint32_t Ln;
     fastc_issue(p, cn, nchunks, lim, lane, nxt, Ln);
@@ -1562,7 +1571,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   if (DRAIN) {
     // the wave's own deferred chunks (its first 64: a wave has ~8; the rest,
     // if any, were flagged for the general kernels above)
-    for (uint64_t m = dmask; m; m &= m - 1) slow_chunk<DMX>(p, T, c_first + (uint32_t)__builtin_ctzll(m) * nw, lane);
+    for (uint64_t m = dmask; m; m &= m - 1) slow_chunk<DMX>(p, T, chunk_of((uint32_t)__builtin_ctzll(m)), lane);
   }
 }
 
@@ -2960,7 +2969,10 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     const uint32_t gcu = fc ? 8u * ncu : ncu;
     if (kf) {
       uint64_t gb = grid_for(kf, wave_blocks, gcu);
-      if (fc && gb < (nchunks + 64u * kWaves - 1) / (64u * kWaves)) gb = (nchunks + 64u * kWaves - 1) / (64u * kWaves);
+      // (a wave takes runs of kRunC chunks: at most 64 / kRunC runs each)
+      const uint64_t runs = (nchunks + kRunC - 1) / kRunC, per = 64u / kRunC;
+      const uint64_t gmin = ((runs + per - 1) / per + kWaves - 1) / kWaves;
+      if (fc && gb < gmin) gb = gmin;
       hipLaunchKernelGGL(kf, dim3((uint32_t)gb), dim3(kBlock), 0, (hipStream_t)stream, p);
     }
   }
