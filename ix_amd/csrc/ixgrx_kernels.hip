@@ -829,6 +829,8 @@ constexpr uint32_t kNoChunk = 0xffffffffu;
 constexpr uint64_t kRun = 64, kRunBig = 1;
 // the coalesced fixed-shape kernel's (fastc_loop)
 constexpr uint32_t kRunC = 2;
+// the span-staged short kernel's (short_span_body)
+constexpr uint32_t kRunS = 1;
 static_assert(64 % kRunC == 0, "whole runs within a wave's 64 drained chunks");
 // big chunks: every frame at least this long (or past the batch end)
 constexpr uint32_t kBigMin = 256;
@@ -1970,14 +1972,16 @@ DEV void short_span_body(const KParams& p) {
   const bool all = mode == IXG_MODE_SHORT;
   if (!all && (mode == IXG_MODE_LONG || p.present[IXG_CLS_SHORT] != p.epoch)) return;  // nothing deferred short
   auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
+  // STRIDED: the wave's j-th chunk is ((j / kRunS) nw + wv) kRunS + j % kRunS
+  // (runs of kRunS consecutive chunks dealt out round-robin)
+  const uint32_t wv = blockIdx.x * W + wave;
+  auto sch = [&](uint32_t j) -> uint64_t { return ((uint64_t)(j / kRunS) * nw + wv) * kRunS + j % kRunS; };
   bool any = all;
-  {
-    const uint32_t wv0 = blockIdx.x * W + wave;
-    for (uint32_t g = STRIDED ? 0u : wv0; !any && (STRIDED ? wv0 + 64u * g * nw < nchunks : g < ngroups);
-         g += STRIDED ? 1u : nw) {
-      const uint32_t ci = STRIDED ? wv0 + (64u * g + (uint32_t)lane) * nw : g * 64u + (uint32_t)lane;
-      any = wave_any(ci < nchunks && mine(ci));
-    }
+  for (uint32_t g = STRIDED ? 0u : wv; !any && (STRIDED ? sch(64u * g) < nchunks : g < ngroups);
+       g += STRIDED ? 1u : nw) {
+    const uint64_t c64 = STRIDED ? sch(64u * g + (uint32_t)lane) : (uint64_t)g * 64u + (uint32_t)lane;
+    const uint32_t ci = c64 < nchunks ? (uint32_t)c64 : 0u;
+    any = wave_any(c64 < nchunks && mine(ci));
   }
   if (!__syncthreads_or(any)) return;
   if (p.tab6) {
@@ -1994,11 +1998,11 @@ DEV void short_span_body(const KParams& p) {
   // so at any moment the grid reads one contiguous window of the batch (a
   // wave per chunk) rather than one region per wave; else wave g takes the
   // 64 consecutive chunks of group g
-  const uint32_t wv = blockIdx.x * W + wave;
-  for (uint32_t g0 = STRIDED ? 0u : wv; STRIDED ? wv + 64u * g0 * nw < nchunks : g0 < ngroups;
+  for (uint32_t g0 = STRIDED ? 0u : wv; STRIDED ? sch(64u * g0) < nchunks : g0 < ngroups;
        g0 += STRIDED ? 1u : nw) {
-    const uint32_t ci = STRIDED ? wv + (64u * g0 + (uint32_t)lane) * nw : g0 * 64u + (uint32_t)lane;
-    const bool want = ci < nchunks && (all || mine(ci));
+    const uint64_t c64 = STRIDED ? sch(64u * g0 + (uint32_t)lane) : (uint64_t)g0 * 64u + (uint32_t)lane;
+    const uint32_t ci = c64 < nchunks ? (uint32_t)c64 : 0u;
+    const bool want = c64 < nchunks && (all || mine(ci));
     const uint64_t m = __ballot(want);
     if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
     const uint32_t nq = (uint32_t)__popcll(m);
