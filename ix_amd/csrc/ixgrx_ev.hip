@@ -59,6 +59,15 @@ DEV Ev classify(const EParams& p, uint32_t i) {
   return e;
 }
 
+// a wave's k-th chunk: runs of kRunE consecutive chunks dealt out
+// round-robin (kRunE = 1: grid-stride)
+constexpr uint32_t kRunE = 1;
+DEV uint32_t ev_chunk(uint32_t k, uint32_t nw, uint32_t nchunks) {
+  const uint32_t w0 = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t c64 = ((uint64_t)(k / kRunE) * nw + w0) * kRunE + k % kRunE;
+  return c64 < nchunks ? (uint32_t)c64 : nchunks;
+}
+
 DEV uint32_t rank_of(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -69,7 +78,7 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_count(EParams p) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < nchunks; c += nw) {
+  for (uint32_t k = 0, c = ev_chunk(0, nw, nchunks); c < nchunks; c = ev_chunk(++k, nw, nchunks)) {
     const Ev e = classify(p, c * 64u + (uint32_t)lane);
     const uint64_t m = __ballot(e.on);
     if (lane == 0) p.chunk_base[c] = (uint32_t)__popcll(m);
@@ -129,7 +138,7 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_emit(EParams p) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  for (uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6); c < nchunks; c += nw) {
+  for (uint32_t k = 0, c = ev_chunk(0, nw, nchunks); c < nchunks; c = ev_chunk(++k, nw, nchunks)) {
     const uint32_t i = c * 64u + (uint32_t)lane;
     const Ev e = classify(p, i);
     const uint64_t m = __ballot(e.on);
