@@ -10,7 +10,7 @@ TAG=${1:-r01}
 O=gpurun_out/$TAG
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
-B="bench.py --steps 20 --warmup 5"
+B="bench.py"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- python3 $B \
   > "$O/bench_under_rocprof.json" 2> "$O/kt.log" || { echo "kernel-trace run failed"; tail -20 "$O/kt.log"; exit 1; }
 python3 tools/kt_summary.py "$O/kt" > "$O/launch_summary.md" || exit 1
