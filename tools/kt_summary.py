@@ -2,9 +2,11 @@
 """Per-launch summary of a `rocprofv3 --kernel-trace --stats` run of bench.py.
 
 One RX launch (ixg_rx_batch_dev / ixg_rx_demux_batch_dev) is a short
-sequence of dispatches on one stream: [ixg_rx_sample] + a fixed-shape kernel
-(ixg_rx_fast*) + the short kernel (ixg_rx_short_*) + the long kernel
-(ixg_rx_general_*); kernels of a class with nothing to do exit at once. The
+sequence of dispatches on one stream: the coalesced fixed-shape kernel
+alone (C2's shape); or the self-sampling short kernel (ixg_rx_short_*) +
+the long kernel (ixg_rx_general_*); or, in forced splits, [ixg_rx_sample] +
+a fixed-shape kernel (ixg_rx_fast*) + the short kernel + the long kernel.
+Kernels of a class with nothing to do exit at once. The
 demux, TX and event kernels are launches of their own. This groups the trace
 into launches, then into runs of consecutive launches with the same kernel
 sequence (bench.py's phases), and prints per run the launch count, the mean
@@ -29,11 +31,17 @@ def launches(rows):
         n = r["Kernel_Name"]
         if n.startswith("ixg_rx"):
             after_sampler = len(cur) == 1 and cur[0]["Kernel_Name"] == "ixg_rx_sample"
-            if cur and (n == "ixg_rx_sample" or (n.startswith("ixg_rx_fast") and not after_sampler)):
+            # the self-sampling short kernel opens a launch of its own
+            # (default plan for offset / wide-stride batches)
+            self_first = n.startswith("ixg_rx_short") and cur and \
+                not cur[-1]["Kernel_Name"].startswith(("ixg_rx_sample", "ixg_rx_fast"))
+            if cur and (n == "ixg_rx_sample" or (n.startswith("ixg_rx_fast") and not after_sampler) or self_first):
                 out.append(cur)
                 cur = []
             cur.append(r)
-            if n.startswith("ixg_rx_general"):
+            # the long kernel ends a launch, and so does the coalesced
+            # fixed-shape kernel in the default plan
+            if n.startswith("ixg_rx_general") or n.startswith("ixg_rx_fastc"):
                 out.append(cur)
                 cur = []
         else:
