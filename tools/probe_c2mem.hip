@@ -7,11 +7,18 @@
 #include <stdint.h>
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int AHEAD>
+// RUN: the wave's k-th chunk is ((k / RUN) nw + w) RUN + k % RUN (the
+// product's coalesced kernel uses RUN = 2)
+template <int AHEAD, int RUN = 1>
 __global__ void __launch_bounds__(256) k_c2(const uint8_t* base, const uint16_t* len, u32x4* out, uint32_t n) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * 4, nch = n / 64;
-  uint32_t c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t w0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+  auto chunk_of = [&](uint32_t k) -> uint32_t {
+    const uint64_t c = ((uint64_t)(k / RUN) * nw + w0) * RUN + k % RUN;
+    return c < nch ? (uint32_t)c : nch;
+  };
+  uint32_t kk = 0, c = chunk_of(0);
   if (c >= nch) return;
   u32x4 v[AHEAD + 1][4];
   uint32_t L[AHEAD + 1];
@@ -26,12 +33,12 @@ __global__ void __launch_bounds__(256) k_c2(const uint8_t* base, const uint16_t*
     l = len[ck * 64u + lane];
   };
 #pragma unroll
-  for (int a = 0; a <= AHEAD; a++) issue(c + a * nw, v[a], L[a]);
+  for (int a = 0; a <= AHEAD; a++) issue(chunk_of(a), v[a], L[a]);
   for (;;) {
     u32x4 acc = v[0][0] ^ v[0][1] ^ v[0][2] ^ v[0][3];
     acc.x ^= L[0];
     __builtin_nontemporal_store(acc, out + (uint64_t)c * 64u + lane);
-    c += nw;
+    c = chunk_of(++kk);
     if (c >= nch) break;
 #pragma unroll
     for (int a = 0; a < AHEAD; a++) {
@@ -39,11 +46,11 @@ __global__ void __launch_bounds__(256) k_c2(const uint8_t* base, const uint16_t*
       for (int k = 0; k < 4; k++) v[a][k] = v[a + 1][k];
       L[a] = L[a + 1];
     }
-    issue(c + AHEAD * nw, v[AHEAD], L[AHEAD]);
+    issue(chunk_of(kk + AHEAD), v[AHEAD], L[AHEAD]);
   }
 }
 
-extern "C" int pm_count(void) { return 4; }
+extern "C" int pm_count(void) { return 7; }
 extern "C" int pm_launch(int w, const void* base, const void* len, void* out, uint32_t n, uint32_t grid, void* s) {
   const uint8_t* b = (const uint8_t*)base;
   const uint16_t* l = (const uint16_t*)len;
@@ -53,5 +60,8 @@ extern "C" int pm_launch(int w, const void* base, const void* len, void* out, ui
   if (w == 1) hipLaunchKernelGGL(k_c2<1>, dim3(grid), dim3(256), 0, st, b, l, o, n);
   if (w == 2) hipLaunchKernelGGL(k_c2<2>, dim3(grid), dim3(256), 0, st, b, l, o, n);
   if (w == 3) hipLaunchKernelGGL(k_c2<3>, dim3(grid), dim3(256), 0, st, b, l, o, n);
+  if (w == 4) hipLaunchKernelGGL((k_c2<1, 2>), dim3(grid), dim3(256), 0, st, b, l, o, n);
+  if (w == 5) hipLaunchKernelGGL((k_c2<2, 2>), dim3(grid), dim3(256), 0, st, b, l, o, n);
+  if (w == 6) hipLaunchKernelGGL((k_c2<3, 2>), dim3(grid), dim3(256), 0, st, b, l, o, n);
   return (int)hipGetLastError();
 }

@@ -24,7 +24,8 @@ def main():
     eng = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags))
     n = wl.n
     s = torch.cuda.current_stream()
-    cfgs = [("product", None, None)] + [(f"ahead{a}_g{g}", a, g) for a in range(4) for g in (1024, 2048, 4096, 8192)]
+    names = ["ahead0", "ahead1", "ahead2", "ahead3", "run2_ahead1", "run2_ahead2", "run2_ahead3"]
+    cfgs = [("product", None, None)] + [(f"{names[a]}_g{g}", a, g) for a in range(7) for g in (2048, 4096, 8192)]
     times = {c[0]: [] for c in cfgs}
     for r in range(10):
         for nm, a, g in cfgs:
