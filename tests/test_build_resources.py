@@ -17,7 +17,7 @@ CSRC = os.path.join(os.path.dirname(HERE), "ix_amd", "csrc")
 HIPCC = "/opt/rocm/bin/hipcc"
 SOURCES = ["ixgrx_kernels.hip", "ixgrx_tx.hip", "ixgrx_demux.hip", "ixgrx_ev.hip"]
 # A/B-only variants (built only with -DIXGRX_AB: tools/build_variant.sh)
-AB_ONLY = re.compile(r"ixg_rx_(general_(w[34]|g16|lt|pk)|short_(w4|spx|[so]$)|fast_a\d|parse|tail)")
+AB_ONLY = re.compile(r"ixg_rx_(general_(w[34]|g16|lt|pk)|short_(w4|spx|[so]$)|fast_a\d|parse|tail|flat_)")
 
 
 def _resources(src):
