@@ -214,7 +214,7 @@ int ixg_rx_set_fdir(void *ctx, const struct ixg_fdir_filter *filters, uint32_t n
  * (each gives bit-identical records, only slower on some layouts). Nothing
  * else (no environment variable) changes the launch plan. */
 enum ixg_split {
-	IXG_SPLIT_AUTO = 0,    /* device-side sampler / coalesced fixed-shape first */
+	IXG_SPLIT_AUTO = 0,    /* mode sampled on the device / coalesced fixed-shape first */
 	IXG_SPLIT_FAST = 1,    /* fixed-shape kernel first, deferred chunks after */
 	IXG_SPLIT_SHORT = 2,   /* short kernel walks every chunk, defers long ones */
 	IXG_SPLIT_LONG = 3,    /* long kernel walks every chunk */
