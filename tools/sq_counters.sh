@@ -12,7 +12,7 @@ for W in $WLS; do
   for k in 1 2; do
     [ $k = 1 ] && C=$P1 || C=$P2
     timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d "$O/${W}_p$k" -o p -- python3 bench.py --workload $W \
-      --secondary "" --extra "" --no-cpu --no-copy --no-demux --no-tx --no-bad --steps 3 --warmup 1 "$@" > "$O/${W}_p$k.json" 2> "$O/${W}_p$k.log" \
+      --secondary "" --extra "" --no-cpu --no-copy --no-demux --no-tx --no-bad --no-strong --steps 3 --warmup 1 "$@" > "$O/${W}_p$k.json" 2> "$O/${W}_p$k.log" \
       || { echo "pass $k $W failed"; tail -20 "$O/${W}_p$k.log"; exit 1; }
   done
 done
