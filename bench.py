@@ -742,10 +742,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    # (the first launches after a batch is built run slower until the
-    # device settles: C2 averaged 0.240 ms over the 20 launches after 5
-    # warm-ups and 0.2166 ms after 20)
-    ap.add_argument("--warmup", type=int, default=30)
+    # (the first launches of a memory-heavy run go through a power-management
+    # transient: C2 runs 0.217 ms for ~8 launches, 0.25 ms around launch 20,
+    # 0.232 ms by launch 40 and ~0.217 ms after that)
+    ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS))
     ap.add_argument("--secondary", default="c4", help="second workload line ('' to skip)")
     ap.add_argument("--extra", default="c3,c5", help="further workload lines (BASELINE configs[2] and [4]; "
