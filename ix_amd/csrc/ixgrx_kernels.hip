@@ -685,6 +685,136 @@ DEV void process_fast(const KParams& p, const uint64_t* __restrict__ T, uint32_t
   }
 }
 
+// Buffer descriptors (gfx950 raw buffers, stride 0): the chunk's base and
+// extent are scalars, each lane's offset a constant, and a piece past the
+// extent reads 0 with no memory access (a store past it is dropped). So a
+// chunk's loads and stores cost no per-lane address arithmetic.
+constexpr int kRsrcWord3 = 0x00020000;  // 32-bit data format, raw addressing
+constexpr int kAuxNT = 2;               // cache policy: nt (streaming)
+DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, kRsrcWord3);
+}
+
+// ---- the lean fixed-shape path (C2's chunks) --------------------------------
+// A one's complement (end-around carry) 32-bit sum, one v_add/v_addc per
+// term: the carry travels between statements in an SGPR pair. Only
+// additions, so the sum is 0 only when every term is 0, and congruent to the
+// exact sum mod 2^32 - 1 (hence mod 0xffff: its 16-bit fold is the exact
+// sum's for any non-zero sum).
+struct Adc {
+  uint32_t acc;
+  uint64_t cc;
+  DEV Adc(uint32_t a, uint32_t b) { asm volatile("v_add_co_u32 %0, %1, %2, %3" : "=v"(acc), "=s"(cc) : "v"(a), "v"(b)); }
+  DEV void add(uint32_t x) { asm volatile("v_addc_co_u32 %0, %1, %0, %2, %1" : "+v"(acc), "+s"(cc) : "v"(x)); }
+  DEV uint32_t end() {
+    asm volatile("v_addc_co_u32 %0, %1, %0, 0, %1" : "+v"(acc), "+s"(cc));
+    return acc;
+  }
+};
+
+// 16-bit fold of a 32-bit one's complement sum (two adds of the halves)
+DEV uint32_t fold32to16(uint32_t x) {
+  x = (x & 0xffffu) + (x >> 16);
+  return (x & 0xffffu) + (x >> 16);
+}
+
+// a ^ b ^ c in one v_bitop3_b32
+DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// A fixed-shape chunk (every frame IPv4 ihl 5 inside 64 bytes, the check of
+// fastc_loop) where, in addition, every frame is a TCP segment tcp_input
+// accepts and all share one IP total length `ipl` (wave-uniform, so the
+// segment end and every byte mask are scalars): C2's chunks, and a stream of
+// 64-byte ACKs in general. Per lane what lane_parse + make_record<true>
+// compute for such a frame, with no per-lane geometry: the IP header sum
+// (bytes 14..33), the L4 sum (bytes 34..e) + pseudo header, the 12 hash
+// lookups, and a verdict that can only be TCP or a checksum drop
+// (ixgbe.c:312-324 then tcp_in.c:189-241). The caller guarantees per lane:
+// proto 6, no fragment bits, 14 + ipl <= L, doff*4 <= ipl - 20 (TCPOK).
+DEV void lean_tcp(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, int lane,
+                  const uint32_t (&d)[kPrefixDw], uint32_t ipl, __amdgpu_buffer_rsrc_t out) {
+  // ---- IP header checksum: hi16(d3) + d4..d7 + lo16(d8) (chksum_internet) ----
+  Adc ip(d[3] >> 16, d[4]);
+  ip.add(d[5]);
+  ip.add(d[6]);
+  ip.add(d[7]);
+  ip.add(d[8] & 0xffffu);
+  const uint32_t ipf = fold32to16(ip.end());
+  const bool ip_ok = ipf == 0xffffu;
+  // ---- L4 sum over [34, e), e = 14 + ipl in [54, 64], plus the pseudo header
+  // (inet_chksum_pseudo_partial): src + dst as 16-bit halves = hi16(d6) +
+  // lo16(d7) + hi16(d7) + lo16(d8), which is congruent mod 0xffff to hi16(d6)
+  // + d7 + lo16(d8); with the segment's hi16(d8) that is d7 + d8 (a 32-bit
+  // word counts as its two halves mod 0xffff). The sum is non-zero (proto
+  // term), so the congruent sum folds to the same 16 bits.
+  const uint32_t e = 14u + ipl;  // scalar
+  const uint32_t l4len = ipl - 20u;
+  auto keep = [](uint32_t x, int t) -> uint32_t {  // scalar mask of the first t bytes
+    return t >= 4 ? x : (t <= 0 ? 0u : x & ((1u << (8 * t)) - 1u));
+  };
+  const uint32_t m13 = keep(~0u, (int)e - 52), m14 = keep(~0u, (int)e - 56), m15 = keep(~0u, (int)e - 60);
+  const uint32_t kps = (6u << 8) + bswap16(l4len);  // htons(proto) + htons(proto_len)
+  Adc l4(d[6] >> 16, d[7]);
+  l4.add(d[8]);
+  l4.add(d[9]);
+  l4.add(d[10]);
+  l4.add(d[11]);
+  l4.add(d[12]);
+  l4.add(d[13] & m13);
+  l4.add(d[14] & m14);
+  l4.add(d[15] & m15);
+  l4.add(kps);
+  const uint32_t l4f = fold32to16(l4.end());
+  const bool l4_ok = l4f == 0xffffu;
+  // ---- Toeplitz + tcp_to_idx: tuple bytes 26..37 (src, dst, sport, dport) ----
+  uint64_t h[12];
+#pragma unroll
+  for (int k = 0; k < 12; k++) h[k] = T[(k << 8) | byte_at(d, 26 + k)];
+  const uint32_t rlo = xor3(xor3((uint32_t)h[0], (uint32_t)h[1], (uint32_t)h[2]),
+                            xor3((uint32_t)h[3], (uint32_t)h[4], (uint32_t)h[5]),
+                            xor3(xor3((uint32_t)h[6], (uint32_t)h[7], (uint32_t)h[8]),
+                                 xor3((uint32_t)h[9], (uint32_t)h[10], (uint32_t)h[11]), 0u));
+  const uint32_t rhi = xor3(xor3((uint32_t)(h[0] >> 32), (uint32_t)(h[1] >> 32), (uint32_t)(h[2] >> 32)),
+                            xor3((uint32_t)(h[3] >> 32), (uint32_t)(h[4] >> 32), (uint32_t)(h[5] >> 32)),
+                            xor3(xor3((uint32_t)(h[6] >> 32), (uint32_t)(h[7] >> 32), (uint32_t)(h[8] >> 32)),
+                                 xor3((uint32_t)(h[9] >> 32), (uint32_t)(h[10] >> 32), (uint32_t)(h[11] >> 32)),
+                                 p.crc_const));
+  uint32_t fg = p.fg_base | (rlo & p.fg_mask);
+  uint32_t flags = IXG_RF_IP_CSUM_CHECKED | IXG_RF_L4_CSUM_CHECKED | IXG_RF_RSS | (ip_ok ? IXG_RF_IP_CSUM_OK : 0u) |
+                   (l4_ok ? IXG_RF_L4_CSUM_OK : 0u);
+  if (p.fdir_mask != 0u) {  // (scalar) flow-director filters installed: the rare path
+    const uint32_t src = (d[6] >> 16) | (d[7] << 16), dst = (d[7] >> 16) | (d[8] << 16);
+    const uint32_t ports = bswap16(d[8] >> 16) | (bswap16(d[9] & 0xffffu) << 16);
+    uint32_t k = ixg_fdir_hash(src, dst, ports) & p.fdir_mask;
+    for (;;) {
+      const u32x4 f = reinterpret_cast<const u32x4*>(p.fdir)[k];
+      if (f.w == 0u) break;
+      if (f.x == src && f.y == dst && f.z == ports) {
+        fg = p.fdir_fg;
+        flags |= IXG_RF_FDIR;
+        break;
+      }
+      k = (k + 1u) & p.fdir_mask;
+    }
+  }
+  // ---- verdict: the driver's checksum drops, else tcp_input's delivery ----
+  const uint32_t doff4 = (d[11] >> 18) & 0x3cu;  // TCPH_HDRLEN * 4 (tcp_in.c:222)
+  const bool drop = !(p.flags & IXG_F_NO_CSUM_DROP) && !(ip_ok && l4_ok);
+  const uint32_t v = drop ? (ip_ok ? IXG_V_DROP_CSUM_L4 : IXG_V_DROP_CSUM_IP) : IXG_V_TCP;
+  Rec r;
+  r.w0 = (fg & 0xffffu) | (v << 16) | (flags << 24);
+  r.w1 = drop ? 0u : ((34u + doff4) | ((l4len - doff4) << 16));
+  r.w2 = rlo;
+  r.w3 = drop ? IXG_NO_BUCKET : ((rhi & (IXG_PCB_BUCKETS - 1)) | (((d[11] >> 24) & 0x3fu) << 16));
+  // (out covers the chunk's valid frames only: the stores of other lanes drop)
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{r.w0, r.w1, r.w2, r.w3}, out, 16 * lane, 0, kAuxNT);
+  if (p.csum && i < p.n) p.csum[i] = ((~ipf) & 0xffffu) | (((~l4f) & 0xffffu) << 16);
+}
+
 // LDS (address space 3) pointers: through generic pointers these would be
 // flat_* accesses, which count on vmcnt as well and force vmcnt(0) waits
 // that serialise the streaming loads.
@@ -1384,27 +1514,27 @@ IXG_FAST_KERNEL(ixg_rx_fast_a1w4_o, true, 1, 4)
 // piece only ever replaces bytes no lane consumes: every byte a lane needs
 // lies below (n-1)*stride + min(L_last, 64) <= lim - 64. A chunk past the
 // end reads the zero page (IXG_ZERO_PAGE = 4096 covers the 4 KiB image).
+// cc, nchunks and lim are wave-uniform (SGPRs)
 DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t lim, int lane, u32x4 (&v)[4],
                      uint32_t& L) {
-  const uint64_t cbase = (uint64_t)cc * 64u * p.stride;
   const bool live = cc < nchunks;
-  const uint8_t* cb = live ? p.base + cbase : p.zero;
-  // the chunk's own 64 * stride bytes only (pieces past them re-read the
-  // last one: no extra traffic); a frame reaching past its chunk (L > stride
-  // in lane 63) is not fixed-shape
-  const uint64_t room = live ? lim - cbase - 16u : 4096u - 16u;
-  const uint32_t cap = 64u * p.stride - 16u;
-  const uint32_t top = room < cap ? (uint32_t)room : cap;
+  const uint64_t cbase = (uint64_t)cc * 64u * p.stride;
+  // the chunk's own 64 * stride bytes only, and nothing past the batch's
+  // readable end (pieces past either read 0: no traffic); a frame reaching
+  // past its chunk (L > stride in lane 63) is not fixed-shape. A chunk past
+  // the end reads nothing.
+  const uint32_t cap = 64u * p.stride;
+  const uint64_t room = live ? lim - cbase : 0u;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(live ? p.base + cbase : p.zero, room < cap ? (uint32_t)room : cap);
 #pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t o = 16u * (uint32_t)(lane + 64 * k);
+  for (int k = 0; k < 4; k++)
     // frames are read once: non-temporal loads (with the nt record stores,
     // 7-8% on C2 over default-policy loads and stores)
-    v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(cb + (o < top ? o : top)));
-  }
-  const uint32_t i = cc * 64u + (uint32_t)lane;
-  const uint32_t ic = i < p.n ? i : p.n - 1;
-  L = p.len[ic];
+    v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * (lane + 64 * k), 0, kAuxNT);
+  // lengths of the chunk's frames (0 past the batch's last)
+  const uint32_t rem = live ? (p.n - cc * 64u < 64u ? p.n - cc * 64u : 64u) : 0u;
+  const __amdgpu_buffer_rsrc_t rl = rsrc(live ? p.len + (uint64_t)cc * 64u : p.len, 2u * rem);
+  L = __builtin_amdgcn_raw_buffer_load_b16(rl, 2 * lane, 0, 0);
 }
 
 // The fused demux of the coalesced kernel, one chunk behind: the chunk's
@@ -1484,7 +1614,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   const uint32_t nchunks = (p.n + 63u) >> 6;
   // the wave's k-th chunk: runs of kRunC consecutive chunks dealt out
   // round-robin (kRunC = 1: grid-stride, the grid reads one window)
-  const uint32_t w0 = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint32_t w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
   auto chunk_of = [&](uint32_t k) -> uint32_t {
     const uint64_t c64 = ((uint64_t)(k / kRunC) * nw + w0) * kRunC + k % kRunC;
     return c64 < nchunks ? (uint32_t)c64 : nchunks;
@@ -1556,7 +1686,15 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
       }
       dmx_issue(p, all_fast && valid, i, r, s.src, s.dst, s.ports, lane, pend);
     } else if (all_fast) {
-      process_fast(p, T, i, valid, Lc, d);
+      // the lean path (lean_tcp) when every frame is a TCP segment
+      // tcp_input accepts and all share one IP total length
+      const uint32_t ipl = __builtin_amdgcn_readfirstlane(ip_len);
+      const bool tcpok = (d[5] & 0xff00ff3fu) == 0x06000000u && 14u + ipl <= Lc &&
+                         ((d[11] >> 18) & 0x3cu) <= ipl - 20u;
+      if (ipl >= 40u && wave_all(!valid || (ip_len == ipl && tcpok)))
+        lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * (p.n - c * 64u < 64u ? p.n - c * 64u : 64u)));
+      else
+        process_fast(p, T, i, valid, Lc, d);
     }
     // the next iteration's LDS writes must not pass this one's reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -286,6 +286,101 @@ def test_fixed_stride_all_fast_and_misaligned_base(engines):
         assert (cs.cpu().numpy().view(np.uint32) == ec).all()
 
 
+def _tcp_frames_uniform(rng, n, ipl, doff, pad_to):
+    """n IPv4/TCP frames with ip_len `ipl`, data offsets `doff` (per frame,
+    any of 0..15: doff*4 > l4len is tcp_input's HDRLEN drop), frame lengths
+    pad_to (per frame, >= 14 + ipl: Ethernet padding past the datagram), valid
+    checksums. Returns (rows [n, 64], lengths)."""
+    rows = np.zeros((n, 64), np.uint8)
+    rows[:, :14 + ipl] = traces.build_ipv4(rng, n, 14 + ipl, 6)
+    traces._put16(rows, 16, np.full(n, ipl))  # (build_ipv4 makes 60-B TCP frames ip_len 40)
+    rows[:, 24:26] = 0
+    traces._put16(rows, 24, (~traces._fold(traces._sum_be16(rows[:, 14:34]))) & 0xFFFF)
+    rows[:, 46] = (doff.astype(np.uint8) << 4)
+    rows[:, 47] = rng.integers(0, 256, n, dtype=np.uint8)  # every TCP flag combination
+    rows[:, 50:52] = 0
+    seg = rows[:, 34:14 + ipl]
+    if seg.shape[1] % 2:
+        seg = np.concatenate([seg, np.zeros((n, 1), np.uint8)], axis=1)
+    s = traces._sum_be16(seg) + traces._sum_be16(rows[:, 26:34]) + 6 + (ipl - 20)
+    traces._put16(rows, 50, (~traces._fold(s)) & 0xFFFF)
+    return rows, pad_to.astype(np.uint16)
+
+
+@pytest.mark.parametrize("S", [60, 64])
+def test_lean_tcp_chunks(S, engines):
+    """The coalesced kernel's lean path (every frame of a chunk an accepted
+    TCP segment of one IP length): chunk-uniform ip_len 40..50, every data
+    offset tcp_input accepts (0 and 5..(ip_len-20)/4), Ethernet padding,
+    every TCP flag byte, bad IP / TCP checksums, the outbound flow director,
+    and chunks that leave the lean path for the general fixed-shape parse:
+    one frame with a data offset past the segment (DROP_TCP_HDRLEN), one UDP
+    frame, one fragment, one frame of another ip_len. Ragged last chunk."""
+    import torch
+    rng = np.random.default_rng(0x1EA0 + S)
+    nch = 160
+    n = 64 * nch - 23
+    ipls = rng.integers(20, 26, nch) * 2  # 40..50, per chunk
+    if S == 60:
+        ipls = np.minimum(ipls, 46)
+    blob = np.zeros(n * S + 128, np.uint8)
+    lens = np.zeros(n, np.uint16)
+    for c in range(nch):
+        m = min(64, n - 64 * c)
+        ipl = int(ipls[c])
+        dmax = (ipl - 20) // 4
+        doff = rng.choice(np.array([0] + list(range(5, dmax + 1))), m)
+        pad = rng.integers(14 + ipl, S + 1, m)
+        rows, L = _tcp_frames_uniform(rng, m, ipl, doff, pad)
+        kind = c % 8
+        if kind == 1:      # data offset past the segment
+            rows[rng.integers(0, m), 46] = 0xF0
+        elif kind == 2:    # a UDP frame
+            rows[rng.integers(0, m), 23] = 17
+        elif kind == 3:    # a fragment
+            rows[rng.integers(0, m), 21] = 0x08
+        elif kind == 4 and ipl < 50 and 14 + ipl + 2 <= S:  # another ip_len
+            j = rng.integers(0, m)
+            r2, _ = _tcp_frames_uniform(rng, 1, ipl + 2, np.array([5]), np.array([14 + ipl + 2]))
+            rows[j] = r2[0]
+            L[j] = max(int(L[j]), 14 + ipl + 2)
+        bad = rng.random(m) < 0.05
+        rows[bad, 24] ^= 0x11
+        bad = rng.random(m) < 0.05
+        rows[bad, 51] ^= 0x22
+        for k in range(m):
+            i = 64 * c + k
+            blob[i * S:i * S + int(L[k])] = rows[k, :int(L[k])]
+        lens[64 * c:64 * c + m] = L
+    tr = traces.Trace(blob, None, lens, S)
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(blob).to(dev)
+    tl = torch.from_numpy(lens.view(np.int16)).to(dev)
+    out = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    cs = torch.empty(n, dtype=torch.int32, device=dev)
+    offs = tr.offsets().astype(np.int64)
+    tcp = np.nonzero(blob[offs + 23] == 6)[0]
+    filt = np.zeros(40, ixgrx.FDIR_DTYPE)
+    pick = rng.choice(tcp, filt.size, replace=False)
+    for k, i in enumerate(pick):
+        o = int(offs[i])
+        filt[k] = (int.from_bytes(bytes(blob[o + 26:o + 30]), "little"), int.from_bytes(bytes(blob[o + 30:o + 34]), "little"),
+                   int(blob[o + 34]) << 8 | int(blob[o + 35]), int(blob[o + 36]) << 8 | int(blob[o + 37]))
+    for flags in (0, ixgrx.IXG_F_NO_CSUM_DROP):
+        eng = engines(flags=flags)
+        for fdir in (None, filt):
+            eng.set_fdir(fdir, 3)
+            try:
+                eng.batch_dev(tb.data_ptr(), None, tl.data_ptr(), S, n, out.data_ptr(), cs.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+                torch.cuda.synchronize()
+            finally:
+                eng.set_fdir(None)
+            er, ec = oracle.rx_batch(KEY, 128, 0, flags, blob, None, lens, S, threads=8, fdir=fdir, cpu_id=3)
+            _diff(out.cpu().numpy(), er, f"lean S={S} flags={flags} fdir={fdir is not None}")
+            assert (cs.cpu().numpy().view(np.uint32) == ec).all()
+
+
 def test_small_stride_with_long_lengths(engines):
     """Fixed stride <= 64 (the coalesced kernel) with some lengths far past
     the stride: those frames read on into their neighbours' bytes, so their
