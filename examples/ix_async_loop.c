@@ -1,0 +1,463 @@
+/*
+ * ix_async_loop.c - IX's run-to-completion loop driving libixgrx's
+ * asynchronous host path, one context per CPU.
+ *
+ * Each thread plays one IX CPU: per iteration of sys_bpoll
+ * (dp/core/syscall.c:134-222) it takes up to eth_rx_max_batch (64) frames off
+ * its RX queue (dp/core/ethqueue.c:71,117-149), hands them to
+ * ixg_rx_submit_mbufs, polls finished records without waiting and runs the
+ * eth_input callees on them through ixg_rx_dispatch, then moves on (timers,
+ * TX). Frames come from an arena of IX mbufs (2112-B elements, len @0, data
+ * @+64) built per thread from a frames file.
+ *
+ * Modes (one JSON line on stdout):
+ *   loop   T threads for S seconds: aggregate Mpkt/s, submit->poll latency
+ *          per iteration (p50/p99/max, us), host-link bytes per frame
+ *   sync   one thread, ixg_rx_batch_mbufs of N frames per call, repeated:
+ *          latency per call (us) and Mpkt/s
+ *   async1 one thread, one batch of N frames at a time: submit, flush,
+ *          poll(wait): the round trip of one batch through the async path
+ *
+ * build: gcc -O2 -Iinclude examples/ix_async_loop.c -Lix_amd -lixgrx -lpthread -o ix_async_loop
+ * usage: ix_async_loop FRAMES_FILE MODE [key=value ...]
+ *   threads=T seconds=S batch=64 n=N arena=FRAMES_PER_THREAD device=D
+ *   cfg_frames= cfg_bytes= cfg_wait_us= cfg_depth= direct=0|1 dump=FILE
+ * FRAMES_FILE: u32 count, u16 lengths[count], then the frames back to back.
+ * dump=FILE (loop mode): thread 0's first `count` records, in submission
+ * order, for the caller's parity check against the oracle.
+ */
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "ixgrx.h"
+
+#define MBUF_STRIDE IXG_MBUF_STRIDE
+
+static double now_s(void)
+{
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+/* ---- options ------------------------------------------------------------- */
+static struct {
+	const char *frames, *mode, *dump;
+	int threads, batch, device, direct;
+	double seconds;
+	uint32_t n, arena;
+	struct ixg_rx_async_cfg acfg;
+} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 2.0, 64, 1u << 16,
+	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, 0}};
+
+static const uint8_t rss_key[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
+				    0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
+				    0x80, 0x30, 0xf2, 0x0c, 0x6a, 0x42, 0xb7, 0x3b, 0xbe, 0xac, 0x01, 0xfa};
+
+/* ---- the frames pool ----------------------------------------------------- */
+static uint32_t pool_n;
+static uint16_t *pool_len;
+static uint8_t **pool_frame;
+static uint64_t pool_bytes;
+
+static int load_pool(const char *path)
+{
+	FILE *f = fopen(path, "rb");
+	if (!f)
+		return -1;
+	if (fread(&pool_n, 4, 1, f) != 1 || pool_n == 0)
+		return -1;
+	pool_len = malloc(pool_n * sizeof(uint16_t));
+	pool_frame = malloc(pool_n * sizeof(uint8_t *));
+	if (!pool_len || !pool_frame || fread(pool_len, 2, pool_n, f) != pool_n)
+		return -1;
+	for (uint32_t i = 0; i < pool_n; i++) {
+		if (pool_len[i] > IXG_MBUF_DATA_LEN)
+			return -1;
+		pool_frame[i] = malloc(pool_len[i] ? pool_len[i] : 1);
+		if (!pool_frame[i] || fread(pool_frame[i], 1, pool_len[i], f) != pool_len[i])
+			return -1;
+		pool_bytes += pool_len[i];
+	}
+	fclose(f);
+	return 0;
+}
+
+/* an arena of n IX mbufs holding the pool tiled: len = size_t at +0, data at
+ * +64 (inc/ix/mbuf.h:73-90) */
+static void **make_arena(uint32_t n, uint8_t **mem)
+{
+	uint8_t *a = aligned_alloc(64, (size_t)n * MBUF_STRIDE);
+	void **p = malloc((size_t)n * sizeof(void *));
+	if (!a || !p)
+		return NULL;
+	for (uint32_t i = 0; i < n; i++) {
+		uint8_t *mb = a + (size_t)i * MBUF_STRIDE;
+		const uint32_t k = i % pool_n;
+		size_t l = pool_len[k];
+		memset(mb, 0, 64);
+		memcpy(mb, &l, sizeof(l));
+		memcpy(mb + 64, pool_frame[k], l);
+		p[i] = mb;
+	}
+	*mem = a;
+	return p;
+}
+
+/* ---- the eth_input callees (counting stand-ins) -------------------------- */
+struct stats {
+	uint64_t tcp, udp, icmp, arp, drop;
+};
+static void on_tcp(void *u, void *m, const struct ixg_rx_rec *r) { (void)m; (void)r; ((struct stats *)u)->tcp++; }
+static void on_udp(void *u, void *m, const struct ixg_rx_rec *r) { (void)m; (void)r; ((struct stats *)u)->udp++; }
+static void on_icmp(void *u, void *m, const struct ixg_rx_rec *r) { (void)m; (void)r; ((struct stats *)u)->icmp++; }
+static void on_arp(void *u, void *m, const struct ixg_rx_rec *r) { (void)m; (void)r; ((struct stats *)u)->arp++; }
+static void on_drop(void *u, void *m, const struct ixg_rx_rec *r) { (void)m; (void)r; ((struct stats *)u)->drop++; }
+static const struct ixg_rx_ops ops = {on_tcp, on_udp, on_icmp, on_arp, on_drop};
+
+static int new_ctx(void **ctx)
+{
+	struct ixg_rx_cfg cfg;
+	memset(&cfg, 0, sizeof(cfg));
+	memcpy(cfg.rss_key, rss_key, 40);
+	cfg.nb_rx_fgs = 128;
+	return ixg_rx_init(&cfg, opt.device, ctx);
+}
+
+static int cmp_d(const void *a, const void *b)
+{
+	const double x = *(const double *)a, y = *(const double *)b;
+	return x < y ? -1 : x > y;
+}
+
+static double pct(double *v, size_t n, double q)
+{
+	if (!n)
+		return 0;
+	size_t k = (size_t)(q * (double)(n - 1) + 0.5);
+	return v[k];
+}
+
+/* ---- loop mode: one thread = one IX CPU --------------------------------- */
+struct worker {
+	int id, rc;
+	pthread_t th;
+	void *ctx;
+	void **ptrs;
+	uint8_t *mem;
+	uint64_t frames_done, iters;
+	double t_end;
+	struct stats st;
+	double *lat;
+	size_t nlat, cap_lat;
+	struct ixg_rx_rec *dump;
+	uint32_t ndump;
+};
+
+static pthread_barrier_t bar;
+static double t_start;
+
+#define POLL_MAX 8192u
+
+static void *work(void *arg)
+{
+	struct worker *w = arg;
+	void **pm = malloc(POLL_MAX * sizeof(void *));
+	struct ixg_rx_rec *pr = malloc(POLL_MAX * sizeof(*pr));
+	/* the iterations in flight: frame sequence number their last frame has,
+	 * and when they were submitted */
+	const size_t qcap = 1u << 20;
+	uint64_t *q_seq = malloc(qcap * sizeof(uint64_t));
+	double *q_t = malloc(qcap * sizeof(double));
+	size_t qh = 0, qt = 0;
+	w->cap_lat = 1u << 22;
+	w->lat = malloc(w->cap_lat * sizeof(double));
+	if (!pm || !pr || !q_seq || !q_t || !w->lat) {
+		w->rc = -12;
+		pthread_barrier_wait(&bar);
+		return NULL;
+	}
+	pthread_barrier_wait(&bar);
+	const uint32_t n = opt.arena;
+	uint64_t sub = 0, got = 0; /* frames submitted / polled */
+	uint32_t pos = 0;
+	for (;;) {
+		const double t = now_s();
+		const int more = t < w->t_end;
+		if (more) {
+			/* one sys_bpoll iteration: up to `batch` frames off the RX queue */
+			uint32_t k = (uint32_t)opt.batch;
+			if (pos + k > n)
+				k = n - pos;
+			int acc = ixg_rx_submit_mbufs(w->ctx, w->ptrs + pos, k);
+			if (acc < 0) {
+				w->rc = acc;
+				break;
+			}
+			if (acc > 0) {
+				sub += (uint64_t)acc;
+				pos = (pos + (uint32_t)acc) % n;
+				if (qt - qh < qcap) {
+					q_seq[qt % qcap] = sub;
+					q_t[qt % qcap] = t;
+					qt++;
+				}
+				w->iters++;
+			}
+		} else if (got == sub) {
+			break;
+		}
+		int r = ixg_rx_poll(w->ctx, pm, pr, POLL_MAX, more ? 0 : 1);
+		if (r < 0) {
+			w->rc = r;
+			break;
+		}
+		if (r > 0) {
+			ixg_rx_dispatch(pm, pr, (uint32_t)r, &ops, &w->st);
+			if (w->dump && w->ndump < pool_n) {
+				uint32_t c = (uint32_t)r < pool_n - w->ndump ? (uint32_t)r : pool_n - w->ndump;
+				memcpy(w->dump + w->ndump, pr, c * sizeof(*pr));
+				w->ndump += c;
+			}
+			got += (uint64_t)r;
+			const double t2 = now_s();
+			while (qh < qt && q_seq[qh % qcap] <= got) {
+				if (w->nlat < w->cap_lat)
+					w->lat[w->nlat++] = (t2 - q_t[qh % qcap]) * 1e6;
+				qh++;
+			}
+		}
+	}
+	w->frames_done = got;
+	free(pm);
+	free(pr);
+	free(q_seq);
+	free(q_t);
+	return NULL;
+}
+
+static int run_loop(void)
+{
+	struct worker *ws = calloc((size_t)opt.threads, sizeof(*ws));
+	if (!ws)
+		return 1;
+	pthread_barrier_init(&bar, NULL, (unsigned)opt.threads + 1);
+	for (int i = 0; i < opt.threads; i++) {
+		struct worker *w = &ws[i];
+		w->id = i;
+		if ((w->rc = new_ctx(&w->ctx)) || (w->rc = ixg_rx_async_init(w->ctx, &opt.acfg))) {
+			fprintf(stderr, "context %d: %s\n", i, ixg_strerror(w->rc));
+			return 2;
+		}
+		w->ptrs = make_arena(opt.arena, &w->mem);
+		if (!w->ptrs)
+			return 1;
+		if (i == 0 && opt.dump)
+			w->dump = malloc(pool_n * sizeof(struct ixg_rx_rec));
+	}
+	/* warm-up: one batch through every context (allocations, code objects) */
+	for (int i = 0; i < opt.threads; i++) {
+		void *pm[64];
+		struct ixg_rx_rec pr[64];
+		ixg_rx_submit_mbufs(ws[i].ctx, ws[i].ptrs, 64);
+		while (ixg_rx_async_pending(ws[i].ctx) > 0)
+			ixg_rx_poll(ws[i].ctx, pm, pr, 64, 1);
+	}
+	t_start = now_s();
+	for (int i = 0; i < opt.threads; i++) {
+		ws[i].t_end = t_start + opt.seconds;
+		pthread_create(&ws[i].th, NULL, work, &ws[i]);
+	}
+	pthread_barrier_wait(&bar);
+	t_start = now_s();
+	for (int i = 0; i < opt.threads; i++)
+		pthread_join(ws[i].th, NULL);
+	const double el = now_s() - t_start;
+	uint64_t frames = 0, iters = 0;
+	struct stats st = {0, 0, 0, 0, 0};
+	size_t nl = 0;
+	for (int i = 0; i < opt.threads; i++) {
+		if (ws[i].rc) {
+			fprintf(stderr, "thread %d: %s\n", i, ixg_strerror(ws[i].rc));
+			return 3;
+		}
+		frames += ws[i].frames_done;
+		iters += ws[i].iters;
+		st.tcp += ws[i].st.tcp;
+		st.udp += ws[i].st.udp;
+		st.icmp += ws[i].st.icmp;
+		st.arp += ws[i].st.arp;
+		st.drop += ws[i].st.drop;
+		nl += ws[i].nlat;
+	}
+	double *lat = malloc((nl ? nl : 1) * sizeof(double));
+	size_t o = 0;
+	for (int i = 0; i < opt.threads; i++) {
+		memcpy(lat + o, ws[i].lat, ws[i].nlat * sizeof(double));
+		o += ws[i].nlat;
+	}
+	qsort(lat, nl, sizeof(double), cmp_d);
+	/* host-link bytes per frame of the staged image: frame bytes past the MAC
+	 * addresses (4-aligned) + the length (+ the offset, non-uniform pools) */
+	uint64_t staged = 0;
+	int uniform = 1;
+	for (uint32_t i = 0; i < pool_n; i++) {
+		staged += pool_len[i] > 12 ? ((pool_len[i] - 12u + 3u) & ~3u) : 0u;
+		uniform &= pool_len[i] == pool_len[0];
+	}
+	const double h2d = (double)staged / pool_n + 2.0 + (uniform ? 0.0 : 8.0);
+	printf("{\"mode\": \"loop\", \"threads\": %d, \"seconds\": %.3f, \"frames\": %llu, \"mpps\": %.2f, "
+	       "\"iterations\": %llu, \"frames_per_iteration\": %.1f, \"batch\": %d, "
+	       "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"n\": %zu}, "
+	       "\"h2d_bytes_per_frame\": %.1f, \"d2h_bytes_per_frame\": 16, "
+	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d}, "
+	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}}\n",
+	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
+	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
+	       nl ? lat[nl - 1] : 0.0, nl, h2d, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
+	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, (unsigned long long)st.tcp,
+	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
+	       (unsigned long long)st.drop);
+	if (opt.dump) {
+		FILE *f = fopen(opt.dump, "wb");
+		if (!f || fwrite(ws[0].dump, sizeof(struct ixg_rx_rec), ws[0].ndump, f) != ws[0].ndump)
+			return 4;
+		fclose(f);
+	}
+	for (int i = 0; i < opt.threads; i++) {
+		ixg_rx_fini(ws[i].ctx);
+		free(ws[i].mem);
+		free(ws[i].ptrs);
+		free(ws[i].lat);
+		free(ws[i].dump);
+	}
+	free(ws);
+	free(lat);
+	return 0;
+}
+
+/* ---- sync / async1 modes: the latency of one batch of n frames ---------- */
+static int run_latency(int async)
+{
+	void *ctx;
+	int rc = new_ctx(&ctx);
+	if (rc || (async && (rc = ixg_rx_async_init(ctx, &opt.acfg)))) {
+		fprintf(stderr, "%s\n", ixg_strerror(rc));
+		return 2;
+	}
+	const uint32_t n = opt.n;
+	uint8_t *mem;
+	void **ptrs = make_arena(n, &mem);
+	struct ixg_rx_rec *recs = malloc((size_t)n * sizeof(*recs));
+	void **pm = malloc((size_t)n * sizeof(void *));
+	if (!ptrs || !recs || !pm)
+		return 1;
+	size_t cap = 200000, nl = 0;
+	double *lat = malloc(cap * sizeof(double));
+	double t0 = 0, tot = 0;
+	for (int it = -3; nl < cap; it++) {
+		const double a = now_s();
+		if (async) {
+			uint32_t i = 0, got = 0;
+			while (i < n) {
+				int acc = ixg_rx_submit_mbufs(ctx, ptrs + i, n - i);
+				if (acc < 0)
+					return 3;
+				i += (uint32_t)acc;
+				if (i < n) { /* ring full: take what is ready */
+					int r = ixg_rx_poll(ctx, pm + got, recs + got, n - got, 1);
+					if (r < 0)
+						return 3;
+					got += (uint32_t)r;
+				}
+			}
+			ixg_rx_flush(ctx);
+			while (got < n) {
+				int r = ixg_rx_poll(ctx, pm + got, recs + got, n - got, 1);
+				if (r < 0)
+					return 3;
+				got += (uint32_t)r;
+			}
+		} else if ((rc = ixg_rx_batch_mbufs(ctx, ptrs, n, recs)) != 0) {
+			fprintf(stderr, "%s\n", ixg_strerror(rc));
+			return 3;
+		}
+		const double b = now_s();
+		if (it < 0)
+			continue; /* warm-up calls */
+		if (nl == 0)
+			t0 = a;
+		lat[nl++] = (b - a) * 1e6;
+		tot += b - a;
+		if (b - t0 > opt.seconds)
+			break;
+	}
+	qsort(lat, nl, sizeof(double), cmp_d);
+	double mean = 0;
+	for (size_t i = 0; i < nl; i++)
+		mean += lat[i];
+	mean /= (double)(nl ? nl : 1);
+	printf("{\"mode\": \"%s\", \"n\": %u, \"calls\": %zu, \"latency_us\": {\"mean\": %.1f, \"p50\": %.1f, "
+	       "\"p99\": %.1f, \"min\": %.1f}, \"mpps\": %.3f, \"direct\": %d}\n",
+	       async ? "async1" : "sync", n, nl, mean, pct(lat, nl, 0.5), pct(lat, nl, 0.99), nl ? lat[0] : 0.0,
+	       (double)n * (double)nl / tot / 1e6, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0);
+	ixg_rx_fini(ctx);
+	free(mem);
+	free(ptrs);
+	free(recs);
+	free(pm);
+	free(lat);
+	return 0;
+}
+
+int main(int argc, char **argv)
+{
+	if (argc < 3) {
+		fprintf(stderr, "usage: %s FRAMES_FILE loop|sync|async1 [key=value ...]\n", argv[0]);
+		return 2;
+	}
+	opt.frames = argv[1];
+	opt.mode = argv[2];
+	for (int i = 3; i < argc; i++) {
+		char *eq = strchr(argv[i], '=');
+		if (!eq)
+			return 2;
+		*eq = 0;
+		const char *k = argv[i], *v = eq + 1;
+		if (!strcmp(k, "threads")) opt.threads = atoi(v);
+		else if (!strcmp(k, "seconds")) opt.seconds = atof(v);
+		else if (!strcmp(k, "batch")) opt.batch = atoi(v);
+		else if (!strcmp(k, "n")) opt.n = (uint32_t)atoi(v);
+		else if (!strcmp(k, "arena")) opt.arena = (uint32_t)atoi(v);
+		else if (!strcmp(k, "device")) opt.device = atoi(v);
+		else if (!strcmp(k, "dump")) opt.dump = v;
+		else if (!strcmp(k, "cfg_frames")) opt.acfg.batch_frames = (uint32_t)atoi(v);
+		else if (!strcmp(k, "cfg_bytes")) opt.acfg.batch_bytes = (uint32_t)atoi(v);
+		else if (!strcmp(k, "cfg_wait_us")) opt.acfg.max_wait_us = (uint32_t)atoi(v);
+		else if (!strcmp(k, "cfg_depth")) opt.acfg.depth = (uint32_t)atoi(v);
+		else if (!strcmp(k, "direct")) opt.acfg.flags = atoi(v) ? IXG_ASYNC_DIRECT : 0;
+		else {
+			fprintf(stderr, "unknown option %s\n", k);
+			return 2;
+		}
+	}
+	if (opt.threads < 1 || opt.batch < 1 || opt.n < 1 || opt.arena < (uint32_t)opt.batch ||
+	    load_pool(opt.frames)) {
+		fprintf(stderr, "bad options or frames file\n");
+		return 2;
+	}
+	if (opt.dump && opt.arena < pool_n)
+		opt.arena = pool_n;
+	if (!strcmp(opt.mode, "loop"))
+		return run_loop();
+	if (!strcmp(opt.mode, "sync"))
+		return run_latency(0);
+	if (!strcmp(opt.mode, "async1"))
+		return run_latency(1);
+	return 2;
+}

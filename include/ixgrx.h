@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define IXGRX_ABI_VERSION 1
+#define IXGRX_ABI_VERSION 2
 
 /* Constants of the reference this ABI is bit-exact against. */
 #define IXG_ETH_MAX_NUM_FG 512u    /* inc/ix/ethfg.h:38 ETH_MAX_NUM_FG */
@@ -166,9 +166,65 @@ int ixg_rx_batch_dev(void *ctx, const struct ixg_rx_frames *frames, uint32_t n,
 
 /* Host batch in IX's own layout: n mbuf pointers (len = size_t at +0, frame
  * data at +64, inc/ix/mbuf.h:73-90). Frames are gathered into pinned
- * staging, copied to the device, processed, and the records copied back to
- * host `out`. Synchronous. 0 or -errno. */
+ * staging without their MAC addresses (bytes 0..11, which nothing on the
+ * path reads), copied to the device as one image per chunk, processed, and
+ * the records copied back to host `out`. Synchronous (pipelined over two
+ * stages for large batches). 0 or -errno. */
 int ixg_rx_batch_mbufs(void *ctx, void *const *mbufs, uint32_t n, struct ixg_rx_rec *out);
+
+/* ---- the asynchronous host path: IX's run loop never waits on the GPU ---- */
+
+/* IX hands at most eth_rx_max_batch (64) frames per sys_bpoll iteration to
+ * eth_input (dp/core/ethqueue.c:71,117-149), then runs timers and TX
+ * (dp/core/syscall.c:187-196). These calls replace that per-packet loop
+ * without a GPU round trip per iteration: submit gathers a CPU's frames of
+ * many iterations into one staged batch (pinned memory, MAC bytes skipped),
+ * which is launched when it is full or its oldest frame has waited
+ * max_wait_us; poll returns finished records, with their mbufs, in the order
+ * the frames were submitted. Neither call waits on the GPU (poll only with
+ * wait != 0). One context per CPU, as everywhere in this ABI. */
+struct ixg_rx_async_cfg {
+	uint32_t batch_frames; /* launch a batch once it holds this many frames */
+	uint32_t batch_bytes;  /* ... or this many frame bytes (>= 4096) */
+	uint32_t max_wait_us;  /* ... or its oldest frame has waited this long
+	                          (checked on every submit and poll) */
+	uint32_t depth;        /* batches in the ring: in flight or not yet
+	                          polled, 1..IXG_ASYNC_MAX_DEPTH */
+	uint32_t flags;        /* IXG_ASYNC_* */
+};
+#define IXG_ASYNC_DIRECT (1u << 0) /* the kernels read the pinned staging and
+                                      write the pinned records themselves
+                                      over the host link: no copies */
+#define IXG_ASYNC_MAX_DEPTH 16u
+#define IXG_ASYNC_DEF_FRAMES 4096u
+#define IXG_ASYNC_DEF_BYTES (2u << 20)
+#define IXG_ASYNC_DEF_WAIT_US 50u
+#define IXG_ASYNC_DEF_DEPTH 8u
+
+/* Configure (or re-configure, with nothing pending) the context's
+ * asynchronous path; cfg NULL = the defaults above. Optional: the first
+ * submit applies the defaults. 0 or -errno (-EBUSY: frames pending). */
+int ixg_rx_async_init(void *ctx, const struct ixg_rx_async_cfg *cfg);
+
+/* Take n mbufs (len @0, data @+64; at most 2048 data bytes each) into the
+ * open batch, launching batches as they fill. Returns the number accepted
+ * (< n when every batch of the ring is in flight or unpolled: poll, then
+ * submit the rest; the caller keeps those mbufs, as IX keeps frames queued
+ * on its RX queue) or -errno. The library keeps the mbuf pointers until poll
+ * returns them and never writes to or frees an mbuf. */
+int ixg_rx_submit_mbufs(void *ctx, void *const *mbufs, uint32_t n);
+
+/* Launch the open batch now (e.g. before idling). 0 or -errno. */
+int ixg_rx_flush(void *ctx);
+
+/* Up to max finished frames, oldest first: mbufs[i] as submitted and its
+ * record recs[i]. wait = 0: never blocks; wait != 0: launches the open batch
+ * and blocks until at least one record is ready (returns 0 at once when
+ * nothing is pending). Returns the count or -errno. */
+int ixg_rx_poll(void *ctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max, int wait);
+
+/* Frames submitted and not yet returned by poll, or -errno. */
+int ixg_rx_async_pending(void *ctx);
 
 /* Host batch from a packed host buffer (same layout rules as
  * ixg_rx_frames, but host pointers). Synchronous. `csum` may be NULL. */
@@ -205,7 +261,13 @@ struct ixg_fdir_filter {
  * outbound_fg_idx() = ETH_MAX_TOTAL_FG + cpu_id (dp/core/ethfg.c:502-505,
  * inc/ix/ethfg.h:135-138). The record carries that fg_id and IXG_RF_FDIR;
  * everything else about the frame is unchanged. cpu_id: the IX CPU the
- * filters steer to (the queue of the CPU that connected). 0 or -errno. */
+ * filters steer to (the queue of the CPU that connected). The table lives in
+ * device memory and the kernels read it at run time, so a launch captured in
+ * a HIP graph sees the current filters, unless the set grew past every
+ * earlier one (the table then moves: capture again). Not concurrently with
+ * this context's launches: the call synchronizes the context's own stream
+ * only, so the caller finishes its launches on other streams first. 0 or
+ * -errno. */
 int ixg_rx_set_fdir(void *ctx, const struct ixg_fdir_filter *filters, uint32_t n, uint16_t cpu_id);
 
 /* How the context's RX launches divide a batch between the kernels

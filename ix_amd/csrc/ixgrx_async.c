@@ -1,0 +1,318 @@
+/*
+ * ixgrx_async.c - the asynchronous, aggregating host path.
+ *
+ * IX's run loop hands at most eth_rx_max_batch (64) frames per sys_bpoll
+ * iteration to eth_input (dp/core/ethqueue.c:71,117-149) and then moves on to
+ * timers and TX (dp/core/syscall.c:187-196). A GPU round trip per 64 frames
+ * would stall that loop for tens of microseconds. Here a context accumulates
+ * the frames of many iterations into one staged batch and launches it when
+ * it is full or its oldest frame has waited long enough; records come back
+ * in submission order on a later poll. The loop never waits on the GPU.
+ *
+ * A context owns a ring of `depth` batches (pinned staging, device image,
+ * a stream, an event and its own defer state each):
+ *
+ *   FREE -> OPEN (frames gathered by submit) -> INFLIGHT (H2D + kernels +
+ *   D2H enqueued) -> DONE (event complete, records being polled) -> FREE
+ *
+ * Batches open, launch and retire in ring order, so records are returned in
+ * the order the frames were submitted.
+ */
+#include <errno.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "ixgrx_ctx.h"
+
+enum { AS_FREE = 0, AS_OPEN, AS_INFLIGHT, AS_DONE };
+
+struct ixg_abatch {
+	int state;
+	struct ixg_dstate ds;
+	hipStream_t stream;
+	hipEvent_t done;
+	uint64_t t_open;     /* ns: when its first frame was gathered */
+	uint32_t n, taken;   /* frames held, frames already returned by poll */
+	size_t span;         /* gathered bytes (ixg_gather_mbufs) */
+	uint8_t *h_buf, *d_buf;
+	uint64_t *h_off;
+	uint16_t *h_len;
+	void **mbufs;
+	struct ixg_rx_rec *h_rec, *d_rec;
+};
+
+struct ixg_async {
+	struct ixg_rx_async_cfg cfg;
+	uint32_t head;       /* oldest batch not yet fully polled */
+	uint32_t tail;       /* next batch to open */
+	uint32_t count;      /* batches in the ring that are not FREE */
+	size_t bytes_cap;    /* gathered-bytes capacity of a batch */
+	struct ixg_abatch b[IXG_ASYNC_MAX_DEPTH];
+};
+
+static uint64_t now_ns(void)
+{
+	struct timespec t;
+	clock_gettime(CLOCK_MONOTONIC, &t);
+	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+static void batch_free(struct ixg_abatch *b)
+{
+	if (b->stream)
+		hipStreamSynchronize(b->stream);
+	ixg_dstate_free(&b->ds);
+	hipHostFree(b->h_buf);
+	hipHostFree(b->h_rec);
+	hipFree(b->d_buf);
+	hipFree(b->d_rec);
+	free(b->h_off);
+	free(b->h_len);
+	free(b->mbufs);
+	if (b->done)
+		hipEventDestroy(b->done);
+	if (b->stream)
+		hipStreamDestroy(b->stream);
+	memset(b, 0, sizeof(*b));
+}
+
+void ixg_async_free(struct ixg_ctx *c)
+{
+	struct ixg_async *a = c->async;
+	if (!a)
+		return;
+	for (uint32_t k = 0; k < IXG_ASYNC_MAX_DEPTH; k++)
+		batch_free(&a->b[k]);
+	free(a);
+	c->async = NULL;
+}
+
+static int batch_alloc(struct ixg_async *a, struct ixg_abatch *b)
+{
+	const uint32_t nf = a->cfg.batch_frames;
+	const size_t bcap = IXG_STAGE_BYTES(a->bytes_cap, nf);
+	HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+	HIPCHK(hipEventCreateWithFlags(&b->done, hipEventDisableTiming));
+	HIPCHK(hipMalloc((void **)&b->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)));
+	HIPCHK(hipMemset(b->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)));
+	HIPCHK(hipHostMalloc((void **)&b->h_buf, bcap, hipHostMallocDefault));
+	HIPCHK(hipHostMalloc((void **)&b->h_rec, (size_t)nf * sizeof(struct ixg_rx_rec), hipHostMallocDefault));
+	if (!(a->cfg.flags & IXG_ASYNC_DIRECT)) {
+		HIPCHK(hipMalloc((void **)&b->d_buf, bcap));
+		HIPCHK(hipMalloc((void **)&b->d_rec, (size_t)nf * sizeof(struct ixg_rx_rec)));
+	}
+	b->h_off = (uint64_t *)malloc((size_t)nf * sizeof(uint64_t));
+	b->h_len = (uint16_t *)malloc((size_t)nf * sizeof(uint16_t));
+	b->mbufs = (void **)malloc((size_t)nf * sizeof(void *));
+	if (!b->h_off || !b->h_len || !b->mbufs)
+		return -ENOMEM;
+	memset(b->h_buf, 0, bcap);
+	return 0;
+}
+
+int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c)
+		return -EINVAL;
+	struct ixg_rx_async_cfg k = {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US,
+				     IXG_ASYNC_DEF_DEPTH, 0};
+	if (cfg)
+		k = *cfg;
+	if (k.batch_frames == 0 || k.batch_frames > (1u << 20) || k.batch_bytes < 4096u ||
+	    k.batch_bytes > (256u << 20) || k.depth < 1 || k.depth > IXG_ASYNC_MAX_DEPTH ||
+	    (k.flags & ~(uint32_t)IXG_ASYNC_DIRECT))
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	if (c->async) {
+		/* re-configuring: only with nothing submitted and not yet polled */
+		if (c->async->count)
+			return -EBUSY;
+		ixg_async_free(c);
+	}
+	struct ixg_async *a = (struct ixg_async *)calloc(1, sizeof(*a));
+	if (!a)
+		return -ENOMEM;
+	a->cfg = k;
+	/* a batch can always take one more frame of the largest size */
+	a->bytes_cap = (size_t)k.batch_bytes + IXG_MBUF_DATA_LEN;
+	c->async = a;
+	for (uint32_t i = 0; i < k.depth; i++) {
+		int rc = batch_alloc(a, &a->b[i]);
+		if (rc) {
+			ixg_async_free(c);
+			return rc;
+		}
+	}
+	return 0;
+}
+
+/* launch the OPEN batch (if any): one H2D image, the kernels, the records
+ * back (or, IXG_ASYNC_DIRECT, kernels reading and writing pinned memory) */
+static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
+{
+	if (!a->count)
+		return 0;
+	const uint32_t last = (a->tail + a->cfg.depth - 1) % a->cfg.depth;
+	struct ixg_abatch *b = &a->b[last];
+	if (b->state != AS_OPEN)
+		return 0;
+	struct ixg_stage st;
+	ixg_stage_finish(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
+	const int direct = (a->cfg.flags & IXG_ASYNC_DIRECT) != 0;
+	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, b->stream);
+	if (rc)
+		return rc;
+	HIPCHK(hipEventRecord(b->done, b->stream));
+	b->state = AS_INFLIGHT;
+	return 0;
+}
+
+/* the batch frames go into: the OPEN one, or a FREE one opened now; NULL
+ * when every batch of the ring is in flight or not yet polled */
+static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
+{
+	if (a->count) {
+		struct ixg_abatch *b = &a->b[(a->tail + a->cfg.depth - 1) % a->cfg.depth];
+		if (b->state == AS_OPEN)
+			return b;
+	}
+	if (a->count == a->cfg.depth)
+		return NULL;
+	struct ixg_abatch *b = &a->b[a->tail];
+	b->state = AS_OPEN;
+	b->t_open = t;
+	b->n = b->taken = 0;
+	b->span = 0;
+	a->tail = (a->tail + 1) % a->cfg.depth;
+	a->count++;
+	return b;
+}
+
+static int due(const struct ixg_async *a, const struct ixg_abatch *b, uint64_t t)
+{
+	return b->n >= a->cfg.batch_frames || b->span >= a->cfg.batch_bytes ||
+	       t - b->t_open >= (uint64_t)a->cfg.max_wait_us * 1000u;
+}
+
+int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (n && !mbufs))
+		return -EINVAL;
+	if (!c->async) {
+		int rc = ixg_rx_async_init(c, NULL);
+		if (rc)
+			return rc;
+	}
+	for (uint32_t i = 0; i < n; i++) {
+		size_t l;
+		memcpy(&l, mbufs[i], sizeof(l));
+		if (l > IXG_MBUF_DATA_LEN) /* an mbuf holds at most 2048 data bytes (mbuf.h) */
+			return -EINVAL;
+	}
+	HIPCHK(hipSetDevice(c->device));
+	struct ixg_async *a = c->async;
+	const uint64_t t = now_ns();
+	uint32_t done = 0;
+	while (done < n) {
+		struct ixg_abatch *b = open_batch(a, t);
+		if (!b)
+			break; /* back-pressure: the caller polls, then submits the rest */
+		/* frames that fit the batch's count and byte limits (the last one
+		 * may pass the byte limit: bytes_cap leaves room for it) */
+		uint32_t m = 0;
+		while (done + m < n && b->n + m < a->cfg.batch_frames && b->span < a->cfg.batch_bytes) {
+			/* at most as many frames as can still start below batch_bytes
+			 * (each stages at most IXG_MBUF_DATA_LEN - 12 bytes) */
+			const size_t room = (a->cfg.batch_bytes - b->span) / (IXG_MBUF_DATA_LEN - 12u) + 1u;
+			uint32_t step = n - done - m < 16u ? n - done - m : 16u;
+			if (step > room)
+				step = (uint32_t)room;
+			const uint32_t take = a->cfg.batch_frames - b->n - m < step ? a->cfg.batch_frames - b->n - m : step;
+			b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, b->h_off + b->n + m,
+						   b->h_len + b->n + m);
+			memcpy(b->mbufs + b->n + m, mbufs + done + m, (size_t)take * sizeof(void *));
+			m += take;
+		}
+		b->n += m;
+		done += m;
+		if (due(a, b, t)) {
+			int rc = launch_open(c, a);
+			if (rc)
+				return rc;
+		}
+	}
+	return (int)done;
+}
+
+int ixg_rx_flush(void *vctx)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c)
+		return -EINVAL;
+	if (!c->async)
+		return 0;
+	HIPCHK(hipSetDevice(c->device));
+	return launch_open(c, c->async);
+}
+
+int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max, int wait)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || (max && (!mbufs || !recs)))
+		return -EINVAL;
+	struct ixg_async *a = c->async;
+	if (!a || !a->count || !max)
+		return 0;
+	HIPCHK(hipSetDevice(c->device));
+	/* an OPEN batch whose oldest frame has waited long enough goes now */
+	{
+		const struct ixg_abatch *o = &a->b[(a->tail + a->cfg.depth - 1) % a->cfg.depth];
+		if (o->state == AS_OPEN && (wait || due(a, o, now_ns()))) {
+			int rc = launch_open(c, a);
+			if (rc)
+				return rc;
+		}
+	}
+	uint32_t got = 0;
+	while (a->count && got < max) {
+		struct ixg_abatch *b = &a->b[a->head];
+		if (b->state == AS_INFLIGHT) {
+			hipError_t e = (wait && got == 0) ? hipEventSynchronize(b->done) : hipEventQuery(b->done);
+			if (e == hipErrorNotReady)
+				break;
+			if (e != hipSuccess)
+				return -EIO;
+			b->state = AS_DONE;
+		}
+		if (b->state != AS_DONE)
+			break; /* the OPEN batch: nothing launched behind it */
+		const uint32_t k = b->n - b->taken < max - got ? b->n - b->taken : max - got;
+		memcpy(mbufs + got, b->mbufs + b->taken, (size_t)k * sizeof(void *));
+		memcpy(recs + got, b->h_rec + b->taken, (size_t)k * sizeof(struct ixg_rx_rec));
+		b->taken += k;
+		got += k;
+		if (b->taken == b->n) {
+			b->state = AS_FREE;
+			a->head = (a->head + 1) % a->cfg.depth;
+			a->count--;
+		}
+	}
+	return (int)got;
+}
+
+int ixg_rx_async_pending(void *vctx)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c)
+		return -EINVAL;
+	const struct ixg_async *a = c->async;
+	if (!a)
+		return 0;
+	uint64_t n = 0;
+	for (uint32_t k = 0, i = a->head; k < a->count; k++, i = (i + 1) % a->cfg.depth)
+		n += a->b[i].n - a->b[i].taken;
+	return n > 0x7fffffffu ? 0x7fffffff : (int)n;
+}

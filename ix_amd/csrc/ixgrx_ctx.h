@@ -1,0 +1,149 @@
+/* ixgrx_ctx.h - the RX context (private to the C host library: ixgrx_host.c,
+ * ixgrx_async.c). */
+#ifndef IXGRX_CTX_H
+#define IXGRX_CTX_H
+
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/ixgrx.h"
+#include "ixgrx_internal.h"
+
+/* per-launch kernel state that concurrent launches must not share: the
+ * defer flags and the class stamps */
+struct ixg_dstate {
+	uint8_t *d_defer;    /* one flag per 64-packet chunk */
+	size_t defer_cap;
+	uint32_t *d_present; /* [IXG_PRESENT_WORDS] (ixg_kparams.present) */
+	uint32_t epoch;      /* last launch's stamp */
+	uint32_t *d_tail;    /* the parse / tail split: 32 B per frame (ixg_kparams.tail) */
+	uint64_t *d_tmeta;   /* 8 B per chunk (ixg_kparams.tmeta) */
+	size_t tail_cap;     /* frames d_tail holds */
+};
+
+/* one stage of the pipelined host path (ixg_rx_batch_mbufs): pinned
+ * staging, device buffers, its own stream and defer state */
+#define IXG_SLOTS 2
+struct ixg_slot {
+	struct ixg_dstate ds;
+	hipStream_t stream;
+	hipEvent_t done;
+	int ready;           /* every buffer below allocated (slot_init) */
+	int busy;            /* work enqueued, records not yet taken */
+	uint32_t first, n;   /* the chunk of the caller's batch it holds */
+	uint8_t *h_buf, *d_buf; /* one H2D image: frames | offsets | lengths (ixg_stage) */
+	uint64_t *h_off;     /* gather scratch */
+	uint16_t *h_len;
+	struct ixg_rx_rec *h_rec, *d_rec;
+};
+
+/* A gathered run laid out for ONE host-to-device copy (ixg_stage_finish):
+ * the frames [0, frames_end) with IXG_TAIL_PAD zero bytes after the last,
+ * then the u64 offsets (packed runs only), then the u16 lengths. A run
+ * whose frames all have one length is a fixed-stride batch (no offsets):
+ * frame k at k * stride, frames running up to 12 bytes into the next slot
+ * (the skipped MAC bytes), which the launch is told (ixg_kparams.overlap). */
+struct ixg_stage {
+	size_t h2d;          /* bytes to copy */
+	size_t o_off, o_len; /* where the offsets / lengths start in the image */
+	uint32_t stride;     /* fixed-stride run: the stride; else 0 */
+};
+/* stage capacity: bytes the image needs for n frames of `span` gathered bytes */
+#define IXG_STAGE_BYTES(span, n) ((((span) + 12u + IXG_TAIL_PAD + 16u) & ~(size_t)7) + (size_t)(n) * 10u)
+
+struct ixg_ctx {
+	int device;
+	struct ixg_rx_cfg cfg;
+	uint32_t crc_const;
+	uint32_t ncu;        /* compute units: persistent grids are sized from it */
+	int force_general;   /* IXG_SPLIT_GENERAL: skip the fixed-shape kernel (ixg_rx_set_split) */
+	int variant;         /* kernel variant selector: 0 in the product library; A/B
+	                        builds (-DIXGRX_AB, tools/build_variant.sh) read it
+	                        from IXGRX_*_VARIANT */
+	uint32_t force_mode; /* IXG_MODE_* forced by ixg_rx_set_split, or IXG_MODE_AUTO */
+	struct ixg_dstate ds; /* the synchronous and device-resident paths' */
+	struct ixg_slot slot[IXG_SLOTS];
+	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
+	uint64_t *d_tab;
+	uint32_t *d_tab6;
+	uint32_t *d_tab32;   /* d_tab split: Toeplitz words, CRC low halves */
+	uint16_t *d_tab16;
+	hipStream_t stream; /* for the synchronous host paths */
+	/* host-path device staging (ixg_rx_batch_host, ixg_demux_batch_host) */
+	uint8_t *d_frames;
+	size_t d_frames_cap;
+	uint64_t *d_off;
+	uint16_t *d_len;
+	struct ixg_rx_rec *d_out;
+	uint32_t *d_csum;
+	size_t d_n_cap;
+	/* PCB demux tables (ixg_demux_load) */
+	int demux_loaded;
+	uint32_t dmx_nfg, dmx_nlisten;
+	uint32_t *d_astart, *d_twstart;
+	struct ixg_pcb_key *d_active, *d_tw;
+	struct ixg_listen_key *d_listen;
+	uint32_t *d_bline;           /* nfg*512 bucket lines of 64 B (ixgrx_walk.h) */
+	struct ixg_demux_rec *d_dmx; /* host-path output staging */
+	size_t d_dmx_cap;
+	/* TX (ixg_tx_set_macs) */
+	uint32_t *d_dmacs;           /* rows of 2 dwords */
+	uint32_t n_dmac;
+	uint32_t smac_lo, smac_hi;
+	uint8_t *d_txbuf, *d_txout;  /* host-path staging */
+	size_t d_txbuf_cap, d_txout_cap;
+	struct ixg_tx_seg *d_txsegs;
+	uint16_t *d_txlen;
+	size_t d_txn_cap;
+	/* event emission scratch: per-chunk counts / bases */
+	uint32_t *d_evbase;
+	size_t evbase_cap;
+	/* flow-director perfect filters (ixg_rx_set_fdir) */
+	uint32_t *d_fdir;            /* header + slots (ixgrx_internal.h); never NULL */
+	size_t fdir_cap;             /* slots d_fdir holds (grow-only)*/
+	/* the asynchronous host path (ixgrx_async.c) */
+	struct ixg_async *async;
+};
+
+
+#define HIPCHK(x)                       \
+	do {                            \
+		if ((x) != hipSuccess)  \
+			return -EIO;    \
+	} while (0)
+
+/* library-internal functions: not exported from libixgrx.so */
+#define IXG_INTERNAL __attribute__((visibility("hidden")))
+
+/* ixgrx_host.c */
+IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
+		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
+		  struct ixg_demux_rec *dmx, uint32_t overlap, hipStream_t s);
+IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
+
+/* The IX-layout gather both host paths use: frames out of mbufs (len =
+ * size_t at +0, data at +64, inc/ix/mbuf.h:73-90) into staging, the MAC
+ * addresses (bytes 0..11, which nothing on the path reads) skipped. Frame k
+ * of the run gets the 4-aligned offset pos[k] and its bytes [12, L) land at
+ * frames + pos[k] + 12; pos[k+1] = pos[k] + round4(max(L, 12) - 12), so a
+ * frame's bytes 0..11 overlap its predecessor's tail. Writes n offsets and
+ * lengths, returns the staged span (pos of the frame after the last). */
+IXG_INTERNAL size_t ixg_gather_mbufs(uint8_t *frames, size_t pos0, void *const *mbufs, uint32_t n, uint64_t *off, uint16_t *len);
+
+IXG_INTERNAL void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint16_t *len, uint32_t n,
+		      struct ixg_stage *st);
+
+/* enqueue one staged image on `s`: its H2D copy, the kernels, the D2H copy
+ * of the records into h_rec; direct: the kernels read the pinned image and
+ * write h_rec themselves (no copies) */
+IXG_INTERNAL int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
+		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
+		     hipStream_t s);
+
+/* ixgrx_async.c */
+IXG_INTERNAL void ixg_async_free(struct ixg_ctx *c);
+
+#endif

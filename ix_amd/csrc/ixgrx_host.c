@@ -5,100 +5,14 @@
  * Plain C over the HIP runtime API; the kernels live in ixgrx_kernels.hip.
  * Semantics of every record field: include/ixgrx.h and DESIGN.md.
  */
-#define __HIP_PLATFORM_AMD__ 1
-#include <hip/hip_runtime_api.h>
-
 #include <errno.h>
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../include/ixgrx.h"
-#include "ixgrx_internal.h"
+#include "ixgrx_ctx.h"
 #include "ixgrx_demux.h"
 #include "ixgrx_tx.h"
 #include "ixgrx_ev.h"
-
-/* per-launch kernel state that concurrent launches must not share: the
- * defer flags and the class stamps */
-struct ixg_dstate {
-	uint8_t *d_defer;    /* one flag per 64-packet chunk */
-	size_t defer_cap;
-	uint32_t *d_present; /* [IXG_PRESENT_WORDS] (ixg_kparams.present) */
-	uint32_t epoch;      /* last launch's stamp */
-	uint32_t *d_tail;    /* the parse / tail split: 32 B per frame (ixg_kparams.tail) */
-	uint64_t *d_tmeta;   /* 8 B per chunk (ixg_kparams.tmeta) */
-	size_t tail_cap;     /* frames d_tail holds */
-};
-
-/* one stage of the pipelined host path (ixg_rx_batch_mbufs): pinned
- * staging, device buffers, its own stream and defer state */
-#define IXG_SLOTS 2
-struct ixg_slot {
-	struct ixg_dstate ds;
-	hipStream_t stream;
-	hipEvent_t done;
-	int ready;           /* every buffer below allocated (slot_init) */
-	int busy;            /* work enqueued, records not yet taken */
-	uint32_t first, n;   /* the chunk of the caller's batch it holds */
-	uint8_t *h_frames, *d_frames;
-	size_t frames_cap;
-	uint64_t *h_off, *d_off;
-	uint16_t *h_len, *d_len;
-	struct ixg_rx_rec *h_rec, *d_rec;
-	size_t n_cap;
-};
-
-struct ixg_ctx {
-	int device;
-	struct ixg_rx_cfg cfg;
-	uint32_t crc_const;
-	uint32_t ncu;        /* compute units: persistent grids are sized from it */
-	int force_general;   /* IXG_SPLIT_GENERAL: skip the fixed-shape kernel (ixg_rx_set_split) */
-	int variant;         /* kernel variant selector: 0 in the product library; A/B
-	                        builds (-DIXGRX_AB, tools/build_variant.sh) read it
-	                        from IXGRX_*_VARIANT */
-	uint32_t force_mode; /* IXG_MODE_* forced by ixg_rx_set_split, or IXG_MODE_AUTO */
-	struct ixg_dstate ds; /* the synchronous and device-resident paths' */
-	struct ixg_slot slot[IXG_SLOTS];
-	uint8_t *d_zero;     /* IXG_ZERO_PAGE bytes of zeros */
-	uint64_t *d_tab;
-	uint32_t *d_tab6;
-	uint32_t *d_tab32;   /* d_tab split: Toeplitz words, CRC low halves */
-	uint16_t *d_tab16;
-	hipStream_t stream; /* for the synchronous host paths */
-	/* host-path device staging (ixg_rx_batch_host, ixg_demux_batch_host) */
-	uint8_t *d_frames;
-	size_t d_frames_cap;
-	uint64_t *d_off;
-	uint16_t *d_len;
-	struct ixg_rx_rec *d_out;
-	uint32_t *d_csum;
-	size_t d_n_cap;
-	/* PCB demux tables (ixg_demux_load) */
-	int demux_loaded;
-	uint32_t dmx_nfg, dmx_nlisten;
-	uint32_t *d_astart, *d_twstart;
-	struct ixg_pcb_key *d_active, *d_tw;
-	struct ixg_listen_key *d_listen;
-	uint32_t *d_bline;           /* nfg*512 bucket lines of 64 B (ixgrx_walk.h) */
-	struct ixg_demux_rec *d_dmx; /* host-path output staging */
-	size_t d_dmx_cap;
-	/* TX (ixg_tx_set_macs) */
-	uint32_t *d_dmacs;           /* rows of 2 dwords */
-	uint32_t n_dmac;
-	uint32_t smac_lo, smac_hi;
-	uint8_t *d_txbuf, *d_txout;  /* host-path staging */
-	size_t d_txbuf_cap, d_txout_cap;
-	struct ixg_tx_seg *d_txsegs;
-	uint16_t *d_txlen;
-	size_t d_txn_cap;
-	/* event emission scratch: per-chunk counts / bases */
-	uint32_t *d_evbase;
-	size_t evbase_cap;
-	/* flow-director perfect filters (ixg_rx_set_fdir) */
-	uint32_t *d_fdir;
-	uint32_t fdir_mask, fdir_fg;
-};
 
 /* ---- hash tables -------------------------------------------------------- */
 
@@ -186,11 +100,17 @@ const char *ixg_strerror(int err)
 	}
 }
 
-#define HIPCHK(x)                       \
-	do {                            \
-		if ((x) != hipSuccess)  \
-			return -EIO;    \
-	} while (0)
+void ixg_dstate_free(struct ixg_dstate *ds)
+{
+	hipFree(ds->d_defer);
+	hipFree(ds->d_tail);
+	hipFree(ds->d_tmeta);
+	hipFree(ds->d_present);
+	memset(ds, 0, sizeof(*ds));
+}
+
+static void ixg_slot_free(struct ixg_slot *sl);
+static int fdir_upload(struct ixg_ctx *c, const uint32_t *tab, uint32_t slots);
 
 void ixg_rx_fini(void *vctx)
 {
@@ -200,36 +120,15 @@ void ixg_rx_fini(void *vctx)
 	hipSetDevice(c->device);
 	if (c->stream)
 		hipStreamSynchronize(c->stream);
+	ixg_async_free(c);
+	for (int k = 0; k < IXG_SLOTS; k++)
+		ixg_slot_free(&c->slot[k]);
 	hipFree(c->d_tab);
 	hipFree(c->d_tab6);
 	hipFree(c->d_tab32);
 	hipFree(c->d_tab16);
-	hipFree(c->ds.d_defer);
-	hipFree(c->ds.d_tail);
-	hipFree(c->ds.d_tmeta);
+	ixg_dstate_free(&c->ds);
 	hipFree(c->d_zero);
-	hipFree(c->ds.d_present);
-	for (int k = 0; k < IXG_SLOTS; k++) {
-		struct ixg_slot *sl = &c->slot[k];
-		if (sl->stream)
-			hipStreamSynchronize(sl->stream);
-		hipFree(sl->ds.d_defer);
-		hipFree(sl->ds.d_tail);
-		hipFree(sl->ds.d_tmeta);
-		hipFree(sl->ds.d_present);
-		hipHostFree(sl->h_frames);
-		hipHostFree(sl->h_off);
-		hipHostFree(sl->h_len);
-		hipHostFree(sl->h_rec);
-		hipFree(sl->d_frames);
-		hipFree(sl->d_off);
-		hipFree(sl->d_len);
-		hipFree(sl->d_rec);
-		if (sl->done)
-			hipEventDestroy(sl->done);
-		if (sl->stream)
-			hipStreamDestroy(sl->stream);
-	}
 	hipFree(c->d_dmacs);
 	hipFree(c->d_bline);
 	hipFree(c->d_txbuf);
@@ -338,6 +237,11 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 		goto fail;
 	if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
 		goto fail;
+	{
+		const uint32_t none[4] = {0, 0, 0, 0};
+		if ((rc = fdir_upload(c, none, 0)) != 0)
+			goto fail;
+	}
 	*out = c;
 	return 0;
 fail:
@@ -347,9 +251,9 @@ fail:
 
 /* ---- batches --------------------------------------------------------------- */
 
-static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
-		     const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
-		     struct ixg_demux_rec *dmx, hipStream_t s)
+int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
+		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
+		  struct ixg_demux_rec *dmx, uint32_t overlap, hipStream_t s)
 {
 	struct ixg_kparams p;
 	memset(&p, 0, sizeof(p));
@@ -370,8 +274,7 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
 	p.zero = c->d_zero;
 	p.fdir = c->d_fdir;
-	p.fdir_mask = c->fdir_mask;
-	p.fdir_fg = c->fdir_fg;
+	p.overlap = overlap;
 	if (dmx) {
 		p.dmx = dmx;
 		p.active_start = c->d_astart;
@@ -420,6 +323,22 @@ static int launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *ba
 	return ixgrx_launch(&p, c->variant, c->ncu, s) == 0 ? 0 : -EIO;
 }
 
+/* the table: header {mask, fg, 0, 0} + slots (ixgrx_internal.h); the
+ * device copy is grow-only, so its address (captured by HIP graphs) only
+ * changes when a larger set arrives */
+static int fdir_upload(struct ixg_ctx *c, const uint32_t *tab, uint32_t slots)
+{
+	if (slots > c->fdir_cap || !c->d_fdir) {
+		hipFree(c->d_fdir);
+		c->d_fdir = NULL;
+		c->fdir_cap = 0;
+		HIPCHK(hipMalloc((void **)&c->d_fdir, ((size_t)slots + 1) * 16));
+		c->fdir_cap = slots;
+	}
+	HIPCHK(hipMemcpy(c->d_fdir, tab, ((size_t)slots + 1) * 16, hipMemcpyHostToDevice));
+	return 0;
+}
+
 int ixg_rx_set_fdir(void *vctx, const struct ixg_fdir_filter *f, uint32_t n, uint16_t cpu_id)
 {
 	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
@@ -427,39 +346,29 @@ int ixg_rx_set_fdir(void *vctx, const struct ixg_fdir_filter *f, uint32_t n, uin
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
 	HIPCHK(hipStreamSynchronize(c->stream));
-	hipFree(c->d_fdir);
-	c->d_fdir = NULL;
-	c->fdir_mask = 0;
-	if (n == 0)
-		return 0;
 	/* open addressing, load factor <= 1/2, linear probing; duplicates kept
 	 * once (a perfect filter matches or not) */
 	uint32_t slots = 16;
 	while (slots < 2 * n)
 		slots <<= 1;
-	uint32_t *tab = (uint32_t *)calloc((size_t)slots * 4, sizeof(uint32_t));
+	uint32_t *tab = (uint32_t *)calloc(((size_t)slots + 1) * 4, sizeof(uint32_t));
 	if (!tab)
 		return -ENOMEM;
+	uint32_t *slot = tab + 4;
 	for (uint32_t i = 0; i < n; i++) {
 		const uint32_t ports = (uint32_t)f[i].src_port | ((uint32_t)f[i].dst_port << 16);
 		uint32_t k = ixg_fdir_hash(f[i].src_ip, f[i].dst_ip, ports) & (slots - 1);
-		while (tab[4 * k + 3] && !(tab[4 * k] == f[i].src_ip && tab[4 * k + 1] == f[i].dst_ip && tab[4 * k + 2] == ports))
+		while (slot[4 * k + 3] &&
+		       !(slot[4 * k] == f[i].src_ip && slot[4 * k + 1] == f[i].dst_ip && slot[4 * k + 2] == ports))
 			k = (k + 1) & (slots - 1);
-		tab[4 * k] = f[i].src_ip;
-		tab[4 * k + 1] = f[i].dst_ip;
-		tab[4 * k + 2] = ports;
-		tab[4 * k + 3] = 1;
+		slot[4 * k] = f[i].src_ip;
+		slot[4 * k + 1] = f[i].dst_ip;
+		slot[4 * k + 2] = ports;
+		slot[4 * k + 3] = 1;
 	}
-	int rc = 0;
-	if (hipMalloc((void **)&c->d_fdir, (size_t)slots * 16) != hipSuccess ||
-	    hipMemcpy(c->d_fdir, tab, (size_t)slots * 16, hipMemcpyHostToDevice) != hipSuccess) {
-		hipFree(c->d_fdir);
-		c->d_fdir = NULL;
-		rc = -ENOMEM;
-	} else {
-		c->fdir_mask = slots - 1;
-		c->fdir_fg = IXG_ETH_MAX_TOTAL_FG + cpu_id;
-	}
+	tab[0] = n ? slots - 1 : 0;
+	tab[1] = IXG_ETH_MAX_TOTAL_FG + cpu_id;
+	const int rc = fdir_upload(c, tab, n ? slots : 0);
 	free(tab);
 	return rc;
 }
@@ -478,7 +387,7 @@ int ixg_rx_set_split(void *vctx, uint32_t split)
 static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
 		  uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum, hipStream_t s)
 {
-	return launch_ds(c, &c->ds, base, off, len, stride, n, out, csum, NULL, s);
+	return ixg_launch_ds(c, &c->ds, base, off, len, stride, n, out, csum, NULL, 0, s);
 }
 
 int ixg_rx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
@@ -573,16 +482,66 @@ int ixg_rx_batch_host(void *vctx, const void *frames, const uint64_t *off, const
 	return 0;
 }
 
-/* The IX-layout host path, pipelined: the batch goes
- * through the device in chunks of at most IXG_PIPE_FRAMES frames /
- * IXG_PIPE_BYTES bytes, alternating between IXG_SLOTS stages, so the CPU
- * gathers chunk k+1 out of the mbufs into pinned staging while chunk k's
- * H2D copy, kernels and D2H copy of records run on the stage's stream (and
- * one stage's D2H overlaps the other's H2D). */
+/* ---- the IX-layout gather ------------------------------ */
+
+size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n, uint64_t *off, uint16_t *len)
+{
+	for (uint32_t k = 0; k < n; k++) {
+		if (k + 6 < n) { /* the mbuf header line (len) and the frame's line */
+			__builtin_prefetch(mbufs[k + 6]);
+			__builtin_prefetch((const uint8_t *)mbufs[k + 6] + IXG_MBUF_HEADER_LEN);
+		}
+		const uint8_t *mb = (const uint8_t *)mbufs[k];
+		size_t l;
+		memcpy(&l, mb, sizeof(l)); /* mbuf->len (inc/ix/mbuf.h:75) */
+		off[k] = pos;
+		len[k] = (uint16_t)l;
+		if (l > 12) {
+			memcpy(frames + pos + 12, mb + IXG_MBUF_HEADER_LEN + 12, l - 12);
+			pos += (l - 12 + 3) & ~(size_t)3;
+		}
+	}
+	return pos;
+}
+
+void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint16_t *len, uint32_t n,
+		      struct ixg_stage *st)
+{
+	const size_t last_end = off[n - 1] + (len[n - 1] > 12 ? len[n - 1] : 12);
+	memset(buf + last_end, 0, IXG_TAIL_PAD + 16);
+	int uniform = 1;
+	for (uint32_t k = 1; k < n && uniform; k++)
+		uniform = len[k] == len[0];
+	const size_t frames_end = (last_end + IXG_TAIL_PAD + 16) & ~(size_t)7;
+	st->o_off = frames_end;
+	if (uniform) {
+		const uint32_t l = len[0] > 12 ? len[0] : 12;
+		const uint32_t stride = (l - 12 + 3) & ~3u;
+		st->stride = stride ? stride : 4;
+		if (!stride) /* frames of <= 12 bytes: nothing staged, slots of 4 zero bytes */
+			memset(buf, 0, (size_t)n * 4 + IXG_TAIL_PAD + 16);
+		st->o_len = frames_end > (size_t)n * 4 + IXG_TAIL_PAD + 16 ? frames_end : ((size_t)n * 4 + IXG_TAIL_PAD + 24) & ~(size_t)7;
+	} else {
+		st->stride = 0;
+		memcpy(buf + st->o_off, off, (size_t)n * sizeof(uint64_t));
+		st->o_len = st->o_off + (size_t)n * sizeof(uint64_t);
+	}
+	memcpy(buf + st->o_len, len, (size_t)n * sizeof(uint16_t));
+	st->h2d = st->o_len + (size_t)n * sizeof(uint16_t);
+	(void)span;
+}
+
+/* ---- the synchronous IX-layout host path ---------------------------------- */
+
+/* ixg_rx_batch_mbufs, pipelined: the batch goes through the device in chunks
+ * of at most IXG_PIPE_FRAMES frames / IXG_PIPE_BYTES gathered bytes,
+ * alternating between IXG_SLOTS stages, so the CPU gathers chunk k+1 out of
+ * the mbufs into pinned staging while chunk k's H2D copy (one per chunk),
+ * kernels and D2H copy of records run on the stage's stream. */
 #define IXG_PIPE_FRAMES 131072u
 #define IXG_PIPE_BYTES (64u << 20)
 
-static int slot_init(struct ixg_ctx *c, struct ixg_slot *sl)
+static int slot_init(struct ixg_slot *sl)
 {
 	/* ready only once every buffer exists: a failed allocation is retried
 	 * on the next call (buffers already made are kept, the rest made) */
@@ -596,28 +555,39 @@ static int slot_init(struct ixg_ctx *c, struct ixg_slot *sl)
 		HIPCHK(hipMalloc((void **)&sl->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 		HIPCHK(hipMemset(sl->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 	}
-	const size_t fcap = IXG_PIPE_BYTES + IXG_TAIL_PAD, ncap = IXG_PIPE_FRAMES;
-	if (!sl->h_frames)
-		HIPCHK(hipHostMalloc((void **)&sl->h_frames, fcap, hipHostMallocDefault));
-	if (!sl->h_off)
-		HIPCHK(hipHostMalloc((void **)&sl->h_off, ncap * sizeof(uint64_t), hipHostMallocDefault));
-	if (!sl->h_len)
-		HIPCHK(hipHostMalloc((void **)&sl->h_len, ncap * sizeof(uint16_t), hipHostMallocDefault));
+	const size_t bcap = IXG_STAGE_BYTES(IXG_PIPE_BYTES + 256u * 2048u, IXG_PIPE_FRAMES), ncap = IXG_PIPE_FRAMES;
+	if (!sl->h_buf)
+		HIPCHK(hipHostMalloc((void **)&sl->h_buf, bcap, hipHostMallocDefault));
+	if (!sl->d_buf)
+		HIPCHK(hipMalloc((void **)&sl->d_buf, bcap));
+	if (!sl->h_off && !(sl->h_off = (uint64_t *)malloc(ncap * sizeof(uint64_t))))
+		return -ENOMEM;
+	if (!sl->h_len && !(sl->h_len = (uint16_t *)malloc(ncap * sizeof(uint16_t))))
+		return -ENOMEM;
 	if (!sl->h_rec)
 		HIPCHK(hipHostMalloc((void **)&sl->h_rec, ncap * sizeof(struct ixg_rx_rec), hipHostMallocDefault));
-	if (!sl->d_frames)
-		HIPCHK(hipMalloc((void **)&sl->d_frames, fcap));
-	if (!sl->d_off)
-		HIPCHK(hipMalloc((void **)&sl->d_off, ncap * sizeof(uint64_t)));
-	if (!sl->d_len)
-		HIPCHK(hipMalloc((void **)&sl->d_len, ncap * sizeof(uint16_t)));
 	if (!sl->d_rec)
 		HIPCHK(hipMalloc((void **)&sl->d_rec, ncap * sizeof(struct ixg_rx_rec)));
-	sl->frames_cap = fcap;
-	sl->n_cap = ncap;
 	sl->ready = 1;
-	(void)c;
 	return 0;
+}
+
+static void ixg_slot_free(struct ixg_slot *sl)
+{
+	if (sl->stream)
+		hipStreamSynchronize(sl->stream);
+	ixg_dstate_free(&sl->ds);
+	hipHostFree(sl->h_buf);
+	hipHostFree(sl->h_rec);
+	hipFree(sl->d_buf);
+	hipFree(sl->d_rec);
+	free(sl->h_off);
+	free(sl->h_len);
+	if (sl->done)
+		hipEventDestroy(sl->done);
+	if (sl->stream)
+		hipStreamDestroy(sl->stream);
+	memset(sl, 0, sizeof(*sl));
 }
 
 /* wait for a stage's chunk and hand its records to the caller */
@@ -625,9 +595,31 @@ static int slot_take(struct ixg_slot *sl, struct ixg_rx_rec *out)
 {
 	if (!sl->busy)
 		return 0;
+	sl->busy = 0;
 	HIPCHK(hipEventSynchronize(sl->done));
 	memcpy(out + sl->first, sl->h_rec, (size_t)sl->n * sizeof(*out));
-	sl->busy = 0;
+	return 0;
+}
+
+/* enqueue one staged image: H2D, kernels, D2H of records (the stream's
+ * work; `dev_frames` is where the image is read from) */
+int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
+		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
+		     hipStream_t s)
+{
+	uint8_t *img = d_buf;
+	if (direct) {
+		img = h_buf; /* the kernels read the pinned image over the host link */
+	} else {
+		HIPCHK(hipMemcpyAsync(d_buf, h_buf, st->h2d, hipMemcpyHostToDevice, s));
+	}
+	int rc = ixg_launch_ds(c, ds, img, st->stride ? NULL : (const uint64_t *)(img + st->o_off),
+			       (const uint16_t *)(img + st->o_len), st->stride, n, direct ? h_rec : d_rec, NULL, NULL,
+			       st->stride ? 1u : 0u, s);
+	if (rc)
+		return rc;
+	if (!direct)
+		HIPCHK(hipMemcpyAsync(h_rec, d_rec, (size_t)n * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s));
 	return 0;
 }
 
@@ -649,38 +641,23 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 	uint32_t i = 0, k = 0;
 	while (i < n && !rc) {
 		struct ixg_slot *sl = &c->slot[k % IXG_SLOTS];
-		if ((rc = slot_init(c, sl)) || (rc = slot_take(sl, out)))
+		if ((rc = slot_init(sl)) || (rc = slot_take(sl, out)))
 			break;
-		/* gather: frame = mbuf + 64, L = mbuf->len (size_t @0), inc/ix/mbuf.h:73-90 */
-		size_t o = 0;
-		uint32_t m = 0;
-		while (i + m < n && m < IXG_PIPE_FRAMES) {
-			const uint8_t *mb = (const uint8_t *)mbufs[i + m];
-			size_t l;
-			memcpy(&l, mb, sizeof(l));
-			const size_t sz = (l + 3) & ~(size_t)3;
-			if (o + sz > IXG_PIPE_BYTES)
-				break;
-			memcpy(sl->h_frames + o, mb + IXG_MBUF_HEADER_LEN, l);
-			memset(sl->h_frames + o + l, 0, sz - l);
-			sl->h_off[m] = o;
-			sl->h_len[m] = (uint16_t)l;
-			o += sz;
-			m++;
+		/* the chunk: at most IXG_PIPE_FRAMES frames, IXG_PIPE_BYTES bytes */
+		uint32_t m = n - i < IXG_PIPE_FRAMES ? n - i : IXG_PIPE_FRAMES;
+		size_t span = 0;
+		uint32_t done = 0;
+		while (done < m && span <= IXG_PIPE_BYTES) {
+			const uint32_t step = m - done < 256u ? m - done : 256u;
+			span = ixg_gather_mbufs(sl->h_buf, span, mbufs + i + done, step, sl->h_off + done, sl->h_len + done);
+			done += step;
 		}
-		memset(sl->h_frames + o, 0, IXG_TAIL_PAD);
-		hipStream_t s = sl->stream;
-		if (hipMemcpyAsync(sl->d_frames, sl->h_frames, o + IXG_TAIL_PAD, hipMemcpyHostToDevice, s) != hipSuccess ||
-		    hipMemcpyAsync(sl->d_off, sl->h_off, m * sizeof(uint64_t), hipMemcpyHostToDevice, s) != hipSuccess ||
-		    hipMemcpyAsync(sl->d_len, sl->h_len, m * sizeof(uint16_t), hipMemcpyHostToDevice, s) != hipSuccess) {
-			rc = -EIO;
+		m = done;
+		struct ixg_stage st;
+		ixg_stage_finish(sl->h_buf, span, sl->h_off, sl->h_len, m, &st);
+		if ((rc = ixg_stage_launch(c, &sl->ds, &st, sl->h_buf, sl->d_buf, m, sl->d_rec, sl->h_rec, 0, sl->stream)))
 			break;
-		}
-		if ((rc = launch_ds(c, &sl->ds, sl->d_frames, sl->d_off, sl->d_len, 0, m, sl->d_rec, NULL, NULL, s)))
-			break;
-		if (hipMemcpyAsync(sl->h_rec, sl->d_rec, m * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s) !=
-			    hipSuccess ||
-		    hipEventRecord(sl->done, s) != hipSuccess) {
+		if (hipEventRecord(sl->done, sl->stream) != hipSuccess) {
 			rc = -EIO;
 			break;
 		}
@@ -858,8 +835,8 @@ int ixg_rx_demux_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t 
 		return -EINVAL;
 	if (hipSetDevice(c->device) != hipSuccess)
 		return -EIO;
-	return launch_ds(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, d_dmx,
-			 (hipStream_t)stream);
+	return ixg_launch_ds(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, d_dmx,
+			     0, (hipStream_t)stream);
 }
 
 int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, const uint16_t *len, uint32_t stride,

@@ -68,12 +68,15 @@ struct ixg_kparams {
 	uint32_t n_listen;
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
-	/* flow director (ixg_rx_set_fdir): open-addressing table of fdir_mask+1
-	 * slots of 4 u32 {src, dst, sport | dport << 16 (host order), 1 = used},
-	 * slot = ixg_fdir_hash(...) & fdir_mask, linear probing; fdir_mask 0 = off */
+	/* flow director (ixg_rx_set_fdir), always present: a header of 4 u32
+	 * {mask, fg = IXG_ETH_MAX_TOTAL_FG + cpu_id, 0, 0} (mask 0 = no filters)
+	 * followed by mask+1 slots of 4 u32 {src, dst, sport | dport << 16 (host
+	 * order), 1 = used}: open addressing, slot = ixg_fdir_hash(...) & mask,
+	 * linear probing */
 	const uint32_t *fdir;
-	uint32_t fdir_mask;
-	uint32_t fdir_fg;      /* IXG_ETH_MAX_TOTAL_FG + cpu_id */
+	uint32_t overlap;      /* fixed-stride batches: frames may run up to 64 bytes
+	                          past their slot (the host paths' staging, whose
+	                          skipped MAC bytes overlap the previous frame) */
 	uint32_t flat_cap;     /* the flat long kernel: 16-byte pieces of LDS per
 	                          wave (set by ixgrx_launch for that kernel) */
 	uint32_t self_sample;  /* set by ixgrx_launch for the span-staged short

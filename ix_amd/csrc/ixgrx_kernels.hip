@@ -277,6 +277,23 @@ struct TabSplit {  // 12 x 256 u32 Toeplitz + 12 x 256 u16 CRC (18 KiB)
 // kShapeAny: anything.
 constexpr int kShapeFixed = 0, kShapeV4 = 1, kShapeV6 = 2, kShapeAny = 3;
 
+// ---- [NIC] flow-director perfect filters (ixg_rx_set_fdir) ----
+// The table lives in device memory with its header (ixgrx_internal.h), read
+// at run time: a graph captured before the filters changed sees the new set.
+// Returns the outbound flow group of a matching frame, or 0xffffffff.
+DEV uint32_t fdir_match(const KParams& p, uint32_t src, uint32_t dst, uint32_t ports) {
+  const u32x4 hdr = *reinterpret_cast<const u32x4*>(p.fdir);  // {mask, fg, 0, 0}: scalar
+  if (hdr.x == 0u) return 0xffffffffu;
+  const u32x4* slot = reinterpret_cast<const u32x4*>(p.fdir) + 1;
+  uint32_t k = ixg_fdir_hash(src, dst, ports) & hdr.x;
+  for (;;) {
+    const u32x4 e = slot[k];
+    if (e.w == 0u) return 0xffffffffu;
+    if (e.x == src && e.y == dst && e.z == ports) return hdr.y;
+    k = (k + 1u) & hdr.x;
+  }
+}
+
 // NDW: prefix dwords available; a segment ending past 4*NDW bytes is left
 // to the streaming rounds.
 template <int SHAPE, int NDW, class Tab, class T6P = const lds_u32*>
@@ -499,17 +516,11 @@ DEV void lane_parse(const KParams& p, const Tab& T, const uint32_t (&d)[kPrefixD
   // IPv4 TCP frame has FLM set, so the driver gives it MBUF_INVALID_FG_ID
   // (ixgbe.c:329-330) and eth_recv_handle_fg_transition the CPU's outbound
   // group (ethfg.c:504-505)
-  if (SHAPE != kShapeV6 && p.fdir_mask != 0u && rss4 && proto == 6u) {
-    uint32_t k = ixg_fdir_hash(src, dst, s.ports) & p.fdir_mask;
-    for (;;) {
-      const u32x4 e = reinterpret_cast<const u32x4*>(p.fdir)[k];
-      if (e.w == 0u) break;
-      if (e.x == src && e.y == dst && e.z == s.ports) {
-        s.fg = p.fdir_fg;
-        s.flags |= IXG_RF_FDIR;
-        break;
-      }
-      k = (k + 1u) & p.fdir_mask;
+  if (SHAPE != kShapeV6 && rss4 && proto == 6u) {
+    const uint32_t g = fdir_match(p, src, dst, s.ports);
+    if (g != 0xffffffffu) {
+      s.fg = g;
+      s.flags |= IXG_RF_FDIR;
     }
   }
 }
@@ -786,19 +797,13 @@ DEV void lean_tcp(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, 
   uint32_t fg = p.fg_base | (rlo & p.fg_mask);
   uint32_t flags = IXG_RF_IP_CSUM_CHECKED | IXG_RF_L4_CSUM_CHECKED | IXG_RF_RSS | (ip_ok ? IXG_RF_IP_CSUM_OK : 0u) |
                    (l4_ok ? IXG_RF_L4_CSUM_OK : 0u);
-  if (p.fdir_mask != 0u) {  // (scalar) flow-director filters installed: the rare path
+  {  // flow-director filters (one scalar header load when none are installed)
     const uint32_t src = (d[6] >> 16) | (d[7] << 16), dst = (d[7] >> 16) | (d[8] << 16);
     const uint32_t ports = bswap16(d[8] >> 16) | (bswap16(d[9] & 0xffffu) << 16);
-    uint32_t k = ixg_fdir_hash(src, dst, ports) & p.fdir_mask;
-    for (;;) {
-      const u32x4 f = reinterpret_cast<const u32x4*>(p.fdir)[k];
-      if (f.w == 0u) break;
-      if (f.x == src && f.y == dst && f.z == ports) {
-        fg = p.fdir_fg;
-        flags |= IXG_RF_FDIR;
-        break;
-      }
-      k = (k + 1u) & p.fdir_mask;
+    const uint32_t g = fdir_match(p, src, dst, ports);
+    if (g != 0xffffffffu) {
+      fg = g;
+      flags |= IXG_RF_FDIR;
     }
   }
   // ---- verdict: the driver's checksum drops, else tcp_input's delivery ----
@@ -1523,7 +1528,9 @@ DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t l
   // readable end (pieces past either read 0: no traffic); a frame reaching
   // past its chunk (L > stride in lane 63) is not fixed-shape. A chunk past
   // the end reads nothing.
-  const uint32_t cap = 64u * p.stride;
+  // (p.overlap: frames run up to 64 bytes past their slot, lane 63's into
+  // the next chunk; the 4 KiB image covers them, stride <= 64)
+  const uint32_t cap = p.overlap ? (p.stride < 63u ? 64u * p.stride + 64u : 4096u) : 64u * p.stride;
   const uint64_t room = live ? lim - cbase : 0u;
   const __amdgpu_buffer_rsrc_t rs = rsrc(live ? p.base + cbase : p.zero, room < cap ? (uint32_t)room : cap);
 #pragma unroll
@@ -1663,7 +1670,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
     const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
     const bool fast = !valid || (Lc <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
-                                 14 + ip_len <= 64 && (lane != 63 || Lc <= p.stride));
+                                 14 + ip_len <= 64 && (lane != 63 || Lc <= p.stride || p.overlap));
     const bool all_fast = wave_all(fast);
     // chunks that are not fixed-shape are finished after the loop (DRAIN)
     // or flagged for the general kernels

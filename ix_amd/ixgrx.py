@@ -17,7 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libixgrx.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 IXG_F_NO_CSUM_DROP = 1 << 0
 IXG_F_IPV6 = 1 << 1
 IXG_TAIL_PAD = 64
@@ -49,6 +49,7 @@ EXPORTS = (
     "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg_rx_demux_batch_dev",
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
     "ixg_ev_batch_dev", "ixg_rx_set_split", "ixg_rx_set_fdir",
+    "ixg_rx_async_init", "ixg_rx_submit_mbufs", "ixg_rx_flush", "ixg_rx_poll", "ixg_rx_async_pending",
 )
 
 # struct ixg_fdir_filter (12 bytes): raw IPs as in the frame, host-order ports
@@ -63,6 +64,16 @@ SPLITS = {"auto": 0, "fast": 1, "short": 2, "long": 3, "general": 4}
 class RxCfg(ctypes.Structure):
     _fields_ = [("rss_key", ctypes.c_uint8 * 40), ("nb_rx_fgs", ctypes.c_uint16),
                 ("dev_idx", ctypes.c_uint16), ("flags", ctypes.c_uint32)]
+
+
+class AsyncCfg(ctypes.Structure):
+    """struct ixg_rx_async_cfg"""
+    _fields_ = [("batch_frames", ctypes.c_uint32), ("batch_bytes", ctypes.c_uint32),
+                ("max_wait_us", ctypes.c_uint32), ("depth", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+IXG_ASYNC_DIRECT = 1 << 0
+ASYNC_DEFAULTS = dict(batch_frames=4096, batch_bytes=2 << 20, max_wait_us=50, depth=8)
 
 
 class RxFrames(ctypes.Structure):
@@ -133,6 +144,16 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_set_split.restype = i32
     lib.ixg_rx_set_fdir.argtypes = [vp, vp, u32, ctypes.c_uint16]
     lib.ixg_rx_set_fdir.restype = i32
+    lib.ixg_rx_async_init.argtypes = [vp, ctypes.POINTER(AsyncCfg)]
+    lib.ixg_rx_async_init.restype = i32
+    lib.ixg_rx_submit_mbufs.argtypes = [vp, vp, u32]
+    lib.ixg_rx_submit_mbufs.restype = i32
+    lib.ixg_rx_flush.argtypes = [vp]
+    lib.ixg_rx_flush.restype = i32
+    lib.ixg_rx_poll.argtypes = [vp, vp, vp, u32, i32]
+    lib.ixg_rx_poll.restype = i32
+    lib.ixg_rx_async_pending.argtypes = [vp]
+    lib.ixg_rx_async_pending.restype = i32
     if lib.ixg_abi_version() != ABI_VERSION:
         raise RuntimeError("libixgrx ABI version mismatch")
     _libs[path] = lib
@@ -225,6 +246,39 @@ class RxEngine:
         _check(self._lib.ixg_rx_batch_mbufs(self._ctx, ptrs.ctypes.data, n, rec.ctypes.data),
                "ixg_rx_batch_mbufs", self._lib)
         return rec
+
+
+    # ---- the asynchronous host path (ixg_rx_submit_mbufs / ixg_rx_poll) ----
+    def async_init(self, batch_frames: int = 4096, batch_bytes: int = 2 << 20, max_wait_us: int = 50,
+                   depth: int = 8, direct: bool = False) -> None:
+        c = AsyncCfg(batch_frames, batch_bytes, max_wait_us, depth, IXG_ASYNC_DIRECT if direct else 0)
+        _check(self._lib.ixg_rx_async_init(self._ctx, ctypes.byref(c)), "ixg_rx_async_init", self._lib)
+
+    def submit_mbufs(self, mbuf_ptrs: np.ndarray) -> int:
+        """Frames accepted (may be fewer than given: poll, then submit the rest)."""
+        ptrs = np.ascontiguousarray(mbuf_ptrs, dtype=np.uint64)
+        rc = self._lib.ixg_rx_submit_mbufs(self._ctx, ptrs.ctypes.data, int(ptrs.shape[0]))
+        if rc < 0:
+            _check(rc, "ixg_rx_submit_mbufs", self._lib)
+        return rc
+
+    def flush(self) -> None:
+        _check(self._lib.ixg_rx_flush(self._ctx), "ixg_rx_flush", self._lib)
+
+    def poll(self, max_frames: int, wait: bool = False) -> tuple[np.ndarray, np.ndarray]:
+        """(mbuf pointers, records) of up to max_frames finished frames, oldest first."""
+        mb = np.zeros(max_frames, dtype=np.uint64)
+        rec = np.zeros(max_frames, dtype=REC_DTYPE)
+        rc = self._lib.ixg_rx_poll(self._ctx, mb.ctypes.data, rec.ctypes.data, max_frames, 1 if wait else 0)
+        if rc < 0:
+            _check(rc, "ixg_rx_poll", self._lib)
+        return mb[:rc], rec[:rc]
+
+    def pending(self) -> int:
+        rc = self._lib.ixg_rx_async_pending(self._ctx)
+        if rc < 0:
+            _check(rc, "ixg_rx_async_pending", self._lib)
+        return rc
 
 
 def make_mbufs(tr) -> tuple[np.ndarray, np.ndarray]:

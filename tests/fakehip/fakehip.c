@@ -1,0 +1,275 @@
+/*
+ * fakehip.c - TEST INFRASTRUCTURE ONLY. A CPU stand-in for the HIP runtime
+ * and the RX kernels, linked with the C host library (ixgrx_host.c,
+ * ixgrx_async.c) into tests/fakehip/libixgrx_fake.so, so the CPU test tier
+ * can drive the host paths' staging, ring and ordering logic (under ASan
+ * and UBSan) without a GPU. Never shipped, never used by a product path.
+ *
+ * "Device" memory is host memory. Every stream is a FIFO of deferred
+ * operations (copies, memsets, launches, event marks) that run only when
+ * someone synchronizes: hipStreamSynchronize and hipEventSynchronize run the
+ * queue up to the point asked for; hipEventQuery returns hipErrorNotReady
+ * the first time it is asked about pending work (and runs nothing), then
+ * runs it. So a host path that read results before synchronizing, or
+ * reused a staging buffer whose copy had not run yet, sees wrong records.
+ * An RX "launch" runs the oracle's restatement (oracle/ixgrx_oracle.c) over
+ * the launch's frames with the configuration fakehip_set_cfg installed.
+ */
+#define __HIP_PLATFORM_AMD__ 1
+#include <hip/hip_runtime_api.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ixgrx.h"
+#include "../../ix_amd/csrc/ixgrx_internal.h"
+#include "../../oracle/ixgrx_oracle.h"
+
+enum { OP_COPY, OP_SET, OP_RX, OP_MARK };
+
+struct op {
+	int kind;
+	void *dst;
+	const void *src;
+	size_t n;
+	int val;
+	struct ixg_kparams p;
+	struct fevent *ev;
+	struct op *next;
+};
+
+struct fstream {
+	struct op *head, *tail;
+};
+
+struct fevent {
+	struct fstream *s; /* stream of the last record, NULL once it ran */
+	int queried;       /* pending work was reported not ready once */
+};
+
+static struct ixg_rx_cfg g_cfg;
+static unsigned long g_launches;
+
+void fakehip_set_cfg(const struct ixg_rx_cfg *cfg) { g_cfg = *cfg; }
+unsigned long fakehip_launches(void) { return g_launches; }
+
+static void run_op(struct op *o)
+{
+	switch (o->kind) {
+	case OP_COPY:
+		memcpy(o->dst, o->src, o->n);
+		break;
+	case OP_SET:
+		memset(o->dst, o->val, o->n);
+		break;
+	case OP_RX: {
+		struct ixg_rx_cfg c = g_cfg;
+		ixgo_rx_batch(&c, o->p.base, o->p.off, o->p.len, o->p.stride, o->p.n, o->p.out, o->p.csum, 1,
+			      IXGO_HASH_TABLE, IXGO_WORK_FULL);
+		g_launches++;
+		break;
+	}
+	case OP_MARK:
+		o->ev->s = NULL;
+		break;
+	}
+}
+
+/* run stream s's operations up to and including `upto` (NULL: all) */
+static void drain(struct fstream *s, struct op *upto)
+{
+	while (s->head) {
+		struct op *o = s->head;
+		s->head = o->next;
+		if (!s->head)
+			s->tail = NULL;
+		run_op(o);
+		const int last = o == upto;
+		free(o);
+		if (last)
+			return;
+	}
+}
+
+static struct fstream g_null;
+static struct fstream *S(hipStream_t s) { return s ? (struct fstream *)s : &g_null; }
+
+static struct op *push(hipStream_t st, struct op *o)
+{
+	struct fstream *s = S(st);
+	o->next = NULL;
+	if (s->tail)
+		s->tail->next = o;
+	else
+		s->head = o;
+	s->tail = o;
+	return o;
+}
+
+static struct op *new_op(int kind)
+{
+	struct op *o = (struct op *)calloc(1, sizeof(*o));
+	if (!o)
+		abort();
+	o->kind = kind;
+	return o;
+}
+
+/* ---- the runtime ---------------------------------------------------------- */
+hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidDevice; }
+hipError_t hipGetDeviceCount(int *n)
+{
+	*n = 1;
+	return hipSuccess;
+}
+hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600 *p, int d)
+{
+	(void)d;
+	memset(p, 0, sizeof(*p));
+	p->multiProcessorCount = 256;
+	return hipSuccess;
+}
+hipError_t hipMalloc(void **p, size_t n)
+{
+	*p = aligned_alloc(256, (n + 255) & ~(size_t)255);
+	return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipHostMalloc(void **p, size_t n, unsigned int f)
+{
+	(void)f;
+	return hipMalloc(p, n);
+}
+hipError_t hipFree(void *p)
+{
+	free(p);
+	return hipSuccess;
+}
+hipError_t hipHostFree(void *p)
+{
+	free(p);
+	return hipSuccess;
+}
+hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind k)
+{
+	(void)k;
+	drain(&g_null, NULL);
+	memcpy(d, s, n);
+	return hipSuccess;
+}
+hipError_t hipMemset(void *d, int v, size_t n)
+{
+	drain(&g_null, NULL);
+	memset(d, v, n);
+	return hipSuccess;
+}
+hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st)
+{
+	(void)k;
+	struct op *o = new_op(OP_COPY);
+	o->dst = d;
+	o->src = s;
+	o->n = n;
+	push(st, o);
+	return hipSuccess;
+}
+hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t st)
+{
+	struct op *o = new_op(OP_SET);
+	o->dst = d;
+	o->val = v;
+	o->n = n;
+	push(st, o);
+	return hipSuccess;
+}
+hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int f)
+{
+	(void)f;
+	*s = (hipStream_t)calloc(1, sizeof(struct fstream));
+	return *s ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipStreamSynchronize(hipStream_t s)
+{
+	drain(S(s), NULL);
+	return hipSuccess;
+}
+hipError_t hipStreamDestroy(hipStream_t s)
+{
+	drain(S(s), NULL);
+	if (s)
+		free(s);
+	return hipSuccess;
+}
+hipError_t hipEventCreateWithFlags(hipEvent_t *e, unsigned int f)
+{
+	(void)f;
+	*e = (hipEvent_t)calloc(1, sizeof(struct fevent));
+	return *e ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipEventDestroy(hipEvent_t e)
+{
+	free(e);
+	return hipSuccess;
+}
+hipError_t hipEventRecord(hipEvent_t e, hipStream_t st)
+{
+	struct fevent *ev = (struct fevent *)e;
+	struct op *o = new_op(OP_MARK);
+	o->ev = ev;
+	ev->s = S(st);
+	ev->queried = 0;
+	push(st, o);
+	return hipSuccess;
+}
+/* run the event's stream up to its (latest) mark */
+static void run_to(struct fevent *ev)
+{
+	struct fstream *s = ev->s;
+	while (ev->s && s->head)
+		drain(s, s->head);
+	ev->s = NULL;
+}
+hipError_t hipEventSynchronize(hipEvent_t e)
+{
+	run_to((struct fevent *)e);
+	return hipSuccess;
+}
+hipError_t hipEventQuery(hipEvent_t e)
+{
+	struct fevent *ev = (struct fevent *)e;
+	if (!ev->s)
+		return hipSuccess;
+	if (!ev->queried) {
+		ev->queried = 1;
+		return hipErrorNotReady;
+	}
+	run_to(ev);
+	return hipSuccess;
+}
+
+/* ---- the kernels' launch entry points (ixgrx_internal.h) ------------------ */
+int ixgrx_launch(const void *params, int variant, uint32_t ncu, void *stream)
+{
+	(void)variant;
+	(void)ncu;
+	struct op *o = new_op(OP_RX);
+	memcpy(&o->p, params, sizeof(o->p));
+	push((hipStream_t)stream, o);
+	return 0;
+}
+uint32_t ixgrx_kparams_size(void) { return (uint32_t)sizeof(struct ixg_kparams); }
+uint32_t ixgrx_block(void) { return 256; }
+int ixgrx_demux_launch(const void *p, uint32_t ncu, void *s)
+{
+	(void)p; (void)ncu; (void)s;
+	return -1;
+}
+int ixgrx_tx_launch(const void *p, uint32_t ncu, void *s)
+{
+	(void)p; (void)ncu; (void)s;
+	return -1;
+}
+int ixgrx_ev_launch(const void *p, uint32_t ncu, void *s)
+{
+	(void)p; (void)ncu; (void)s;
+	return -1;
+}

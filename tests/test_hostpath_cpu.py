@@ -1,0 +1,196 @@
+"""The host paths' own logic on the CPU (no GPU): the C host library
+(ixgrx_host.c, ixgrx_async.c) linked with tests/fakehip/fakehip.c, a CPU
+stand-in for the HIP runtime whose streams defer every copy and launch until
+someone synchronizes, and whose RX launch runs the oracle. What this covers:
+the MAC-skipping gather, the staged image (fixed-stride and offset layouts),
+the asynchronous ring (open / in flight / done, back-pressure, flush,
+ordering) and the synchronous pipelined path; any read of results before
+synchronizing, or reuse of a buffer whose copy has not run, shows up as
+wrong records. tests/test_sanitize.py re-runs this file against the
+ASan/UBSan build. The kernels themselves are the -m gpu tests' business."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from ix_amd import ixgrx, traces
+from oracle import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FAKE = os.path.join(ROOT, "build", "fakehip", "libixgrx_fake.so")
+KEY = traces.RSS_KEY
+
+
+@pytest.fixture(scope="module")
+def fake():
+    path = os.environ.get("IXG_FAKE_LIB")
+    if not path:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "fakehip")], check=True)
+        path = FAKE
+    lib = ixgrx.load_library(path)
+    lib.fakehip_set_cfg.argtypes = [ctypes.POINTER(ixgrx.RxCfg)]
+    lib.fakehip_launches.restype = ctypes.c_ulong
+
+    def engine(flags=0, nb=128, dev=0):
+        cfg = ixgrx.Config(KEY, nb, dev, flags)
+        c = cfg.to_c()
+        lib.fakehip_set_cfg(ctypes.byref(c))
+        return ixgrx.RxEngine(cfg, lib_path=path)
+    engine.lib = lib
+    return engine
+
+
+def _mbufs(kind, n, seed):
+    tr = traces.make_trace(kind, n, seed=seed, bad_ip=0.02, bad_l4=0.02)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    return tr, arena, ptrs
+
+
+def _expect(ptrs, flags=0):
+    return oracle.rx_mbufs(KEY, 128, 0, flags, ptrs, threads=8)
+
+
+@pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed", "tcp1514"])
+def test_sync_mbufs(fake, kind):
+    tr, arena, ptrs = _mbufs(kind, 3000, seed=7)
+    eng = fake()
+    try:
+        rec = eng.batch_mbufs(ptrs)
+    finally:
+        eng.close()
+    assert np.array_equal(rec.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+
+
+def test_sync_mbufs_pipelined(fake):
+    """More frames than one pipeline chunk (131072): both stages, in turn."""
+    tr, arena, ptrs = _mbufs("tcp64", 300000, seed=8)
+    eng = fake()
+    try:
+        rec = eng.batch_mbufs(ptrs)
+        rec2 = eng.batch_mbufs(ptrs[:1000])
+    finally:
+        eng.close()
+    exp = _expect(ptrs)
+    assert np.array_equal(rec.view(np.uint8).reshape(-1, 16), exp)
+    assert np.array_equal(rec2.view(np.uint8).reshape(-1, 16), exp[:1000])
+
+
+def test_tiny_frames(fake):
+    """Frames of 0..13 bytes (nothing or one byte past the MACs staged), in
+    a batch of one length (fixed-stride staging) and mixed."""
+    rng = np.random.default_rng(3)
+    for lens in ([5] * 300, list(rng.integers(0, 14, 500)), [12] * 70, [13] * 65):
+        frames = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in lens]
+        tr = traces.pack(frames)
+        arena, ptrs = ixgrx.make_mbufs(tr)
+        eng = fake()
+        try:
+            rec = eng.batch_mbufs(ptrs)
+        finally:
+            eng.close()
+        assert np.array_equal(rec.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+
+
+def _loop(eng, ptrs, rng, max_batch=64):
+    got_m, got_r = [], []
+    i = 0
+    while i < len(ptrs):
+        k = int(rng.integers(1, max_batch + 1))
+        acc = eng.submit_mbufs(ptrs[i:i + k])
+        assert 0 <= acc <= k
+        i += acc
+        m, r = eng.poll(1000, wait=acc == 0)
+        got_m.append(m)
+        got_r.append(r)
+    while eng.pending():
+        m, r = eng.poll(1000, wait=True)
+        got_m.append(m)
+        got_r.append(r)
+    return np.concatenate(got_m), np.concatenate(got_r)
+
+
+@pytest.mark.parametrize("kind,cfg", [
+    ("imix", dict()),
+    ("tcp64", dict(batch_frames=1000, depth=2)),
+    ("mixed", dict(batch_frames=4096, max_wait_us=0)),
+    ("imix", dict(batch_frames=64, depth=1)),
+    ("tcp1514", dict(batch_frames=300, batch_bytes=64 << 10, depth=3)),
+    ("imix", dict(batch_frames=4096, batch_bytes=4096, depth=16)),
+    ("tcp64", dict(batch_frames=100, depth=4, direct=True)),
+])
+def test_async_submit_poll(fake, kind, cfg):
+    rng = np.random.default_rng(len(cfg) + len(kind))
+    tr, arena, ptrs = _mbufs(kind, 12000, seed=9)
+    eng = fake()
+    try:
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, **cfg})
+        m, r = _loop(eng, ptrs, rng)
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+
+
+def test_async_aggregates_iterations(fake):
+    """64-frame submissions are aggregated: 100 iterations of 64 frames with
+    batch_frames 1600 make 4 launches, not 100."""
+    tr, arena, ptrs = _mbufs("tcp64", 6400, seed=10)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=1600, batch_bytes=1 << 24, max_wait_us=10000000, depth=8)
+        n0 = fake.lib.fakehip_launches()
+        for k in range(100):
+            assert eng.submit_mbufs(ptrs[64 * k:64 * k + 64]) == 64
+        m, r = eng.poll(10000, wait=True)
+        while eng.pending():
+            m2, r2 = eng.poll(10000, wait=True)
+            m, r = np.concatenate([m, m2]), np.concatenate([r, r2])
+        assert fake.lib.fakehip_launches() - n0 == 4
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+
+
+def test_async_back_pressure_flush_and_busy(fake):
+    tr, arena, ptrs = _mbufs("imix", 400, seed=11)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=64, batch_bytes=1 << 20, max_wait_us=10000000, depth=1)
+        assert eng.submit_mbufs(ptrs[:200]) == 64
+        assert eng.submit_mbufs(ptrs[64:200]) == 0
+        assert eng.pending() == 64
+        m, r = eng.poll(1000, wait=False)  # not ready on the first look
+        assert m.size == 0
+        m, r = eng.poll(1000, wait=True)
+        assert np.array_equal(m, ptrs[:64])
+        assert eng.submit_mbufs(ptrs[64:100]) == 36
+        assert eng.poll(1000)[0].size == 0 and eng.pending() == 36
+        with pytest.raises(RuntimeError, match="ixg_rx_async_init"):
+            eng.async_init(batch_frames=10)
+        eng.flush()
+        m3, r3 = eng.poll(1000, wait=True)
+        assert np.array_equal(m3, ptrs[64:100]) and eng.pending() == 0
+        eng.async_init(batch_frames=10, depth=2)  # nothing pending: re-configure
+        assert eng.submit_mbufs(ptrs[100:125]) == 20  # two batches of 10, then back-pressure
+    finally:
+        eng.close()
+    exp = _expect(ptrs[:100])
+    assert np.array_equal(np.concatenate([r, r3]).view(np.uint8).reshape(-1, 16), exp)
+
+
+def test_async_rejects_oversized_and_bad_cfg(fake):
+    tr, arena, ptrs = _mbufs("tcp64", 10, seed=12)
+    arena[(int(ptrs[3]) - arena.ctypes.data):][:8] = np.frombuffer(np.uint64(2049).tobytes(), np.uint8)
+    eng = fake()
+    try:
+        with pytest.raises(RuntimeError, match="ixg_rx_submit_mbufs"):
+            eng.submit_mbufs(ptrs)
+        assert eng.pending() == 0
+        for bad in (dict(batch_frames=0), dict(depth=0), dict(depth=17), dict(batch_bytes=100)):
+            with pytest.raises(RuntimeError, match="ixg_rx_async_init"):
+                eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, **bad})
+    finally:
+        eng.close()

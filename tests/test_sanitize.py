@@ -1,8 +1,9 @@
 """Host sanitizers: the C host library (ix_amd/csrc/ixgrx_host.c)
 and the oracle (oracle/ixgrx_oracle.c) built with -fsanitize=address,undefined,
 and the CPU test tier re-run against those builds in a child process with the
-sanitizer runtimes preloaded. The two C examples are built against the
-sanitized host library and run too (on a machine without a GPU they stop at
+sanitizer runtimes preloaded. The host paths' staging and ring logic runs
+sanitized over the CPU stand-in for HIP (tests/fakehip). The two C examples
+are built against the sanitized host library and run too (on a machine without a GPU they stop at
 ixg_rx_init's -ENODEV, after exercising argument checking and context setup).
 
 Any ASan report or UBSan error aborts the child (-fno-sanitize-recover), so
@@ -17,6 +18,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SAN_LIB = os.path.join(ROOT, "build", "san", "libixgrx.so")
 SAN_ORACLE = os.path.join(ROOT, "oracle", "_san", "liboracle.so")
+SAN_FAKE = os.path.join(ROOT, "build", "fakehip", "libixgrx_fake_san.so")
 
 
 def _runtime(name):
@@ -33,7 +35,8 @@ def san_build():
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "san"], check=True)
     subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "ix_amd", "csrc"), "san"], check=True,
                    capture_output=True)
-    assert os.path.exists(SAN_LIB) and os.path.exists(SAN_ORACLE)
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "fakehip")], check=True, capture_output=True)
+    assert os.path.exists(SAN_LIB) and os.path.exists(SAN_ORACLE) and os.path.exists(SAN_FAKE)
 
 
 def _env():
@@ -43,6 +46,7 @@ def _env():
     env["UBSAN_OPTIONS"] = "print_stacktrace=1:halt_on_error=1"
     env["IXG_SAN_LIB"] = SAN_LIB        # tests/conftest.py swaps these builds in
     env["IXG_SAN_ORACLE"] = SAN_ORACLE
+    env["IXG_FAKE_LIB"] = SAN_FAKE       # tests/test_hostpath_cpu.py: the host paths over fakehip
     return env
 
 
@@ -60,7 +64,7 @@ def test_cpu_tier_under_sanitizers(san_build):
     ABI's host-side entry points, TX/demux/event oracles), with both C
     libraries replaced by their sanitized builds."""
     tests = ["test_oracle_golden.py", "test_abi.py", "test_tx.py", "test_demux.py", "test_events.py",
-             "test_traces.py"]
+             "test_traces.py", "test_hostpath_cpu.py"]
     cmd = [sys.executable, "-m", "pytest", "-q", "-x", "-m", "not gpu", "-p", "no:cacheprovider"] + \
         [os.path.join(ROOT, "tests", t) for t in tests]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=_env(), cwd=ROOT)
