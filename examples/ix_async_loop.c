@@ -53,7 +53,7 @@ static struct {
 	uint32_t n, arena;
 	struct ixg_rx_async_cfg acfg;
 } opt = {NULL, "loop", NULL, 1, 64, 0, 0, 2.0, 64, 1u << 16,
-	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, 0}};
+	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}};
 
 static const uint8_t rss_key[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
 				    0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,

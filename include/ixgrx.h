@@ -196,10 +196,11 @@ struct ixg_rx_async_cfg {
                                       write the pinned records themselves
                                       over the host link: no copies */
 #define IXG_ASYNC_MAX_DEPTH 16u
-#define IXG_ASYNC_DEF_FRAMES 4096u
-#define IXG_ASYNC_DEF_BYTES (2u << 20)
+#define IXG_ASYNC_DEF_FRAMES 16384u
+#define IXG_ASYNC_DEF_BYTES (4u << 20)
 #define IXG_ASYNC_DEF_WAIT_US 50u
-#define IXG_ASYNC_DEF_DEPTH 8u
+#define IXG_ASYNC_DEF_DEPTH 3u
+#define IXG_ASYNC_DEF_FLAGS IXG_ASYNC_DIRECT
 
 /* Configure (or re-configure, with nothing pending) the context's
  * asynchronous path; cfg NULL = the defaults above. Optional: the first

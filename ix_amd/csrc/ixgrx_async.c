@@ -117,7 +117,7 @@ int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
 	if (!c)
 		return -EINVAL;
 	struct ixg_rx_async_cfg k = {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US,
-				     IXG_ASYNC_DEF_DEPTH, 0};
+				     IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS};
 	if (cfg)
 		k = *cfg;
 	if (k.batch_frames == 0 || k.batch_frames > (1u << 20) || k.batch_bytes < 4096u ||

@@ -51,6 +51,8 @@ def _run_loop(eng, ptrs, rng, max_batch=64, poll_every=1):
     ("tcp64", dict(batch_frames=1000, depth=2)),                 # uniform lengths: fixed-stride staging
     ("mixed", dict(batch_frames=4096, max_wait_us=0)),           # every submit launches (no aggregation)
     ("imix", dict(batch_frames=64, depth=1)),                    # back-pressure: one batch in the ring
+    ("imix", dict(batch_frames=4096, depth=8, direct=False)),    # staged copies (H2D image, D2H records)
+    ("tcp64", dict(batch_frames=1000, depth=2, direct=False)),
     ("tcp1514", dict(batch_frames=300, batch_bytes=64 << 10, depth=3)),  # the byte limit closes batches
     ("imix", dict(batch_frames=2048, depth=4, direct=True)),     # kernels on pinned host memory
     ("tcp64", dict(batch_frames=512, depth=4, direct=True)),

@@ -116,6 +116,8 @@ def _loop(eng, ptrs, rng, max_batch=64):
     ("tcp64", dict(batch_frames=1000, depth=2)),
     ("mixed", dict(batch_frames=4096, max_wait_us=0)),
     ("imix", dict(batch_frames=64, depth=1)),
+    ("imix", dict(batch_frames=4096, depth=8, direct=False)),     # staged copies (H2D image, D2H records)
+    ("tcp64", dict(batch_frames=1000, depth=2, direct=False)),
     ("tcp1514", dict(batch_frames=300, batch_bytes=64 << 10, depth=3)),
     ("imix", dict(batch_frames=4096, batch_bytes=4096, depth=16)),
     ("tcp64", dict(batch_frames=100, depth=4, direct=True)),
