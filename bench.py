@@ -655,6 +655,18 @@ def host_path(seconds: float = 3.0, threads=(1, 4, 16)):
         res["loop"][f"threads{t}"] = _loop_run(fpath, "loop", 300, **kw)
         if t == threads[0] and os.path.exists(dump):
             recs = np.fromfile(dump, dtype=np.uint8).reshape(-1, 16)
+    # zero copy: the mbuf arenas registered, the kernels read the frames in
+    # place over the host link (ixg_rx_register_memory)
+    dump_zc = os.path.join(tmp, "dump_zc.bin")
+    for t in threads:
+        kw = dict(threads=t, seconds=seconds, batch=64, arena=1 << 17, register=1)
+        if t == threads[0]:
+            kw["dump"] = dump_zc
+        res["loop"][f"threads{t}_zero_copy"] = _loop_run(fpath, "loop", 300, **kw)
+    if recs is not None and os.path.exists(dump_zc):
+        zc = np.fromfile(dump_zc, dtype=np.uint8).reshape(-1, 16)
+        if not np.array_equal(zc, recs):
+            recs = None  # the two passes must agree (and then both match the oracle)
     if recs is not None and recs.shape[0] == pool.n:
         check = ("hostpath", pool, recs)
         res["parity"] = "pending oracle"

@@ -22,6 +22,8 @@
  * usage: ix_async_loop FRAMES_FILE MODE [key=value ...]
  *   threads=T seconds=S batch=64 n=N arena=FRAMES_PER_THREAD device=D
  *   cfg_frames= cfg_bytes= cfg_wait_us= cfg_depth= direct=0|1 dump=FILE
+ *   register=1: register each thread's mbuf arena (ixg_rx_register_memory)
+ *   so the kernels read the frames in place (zero copy)
  * FRAMES_FILE: u32 count, u16 lengths[count], then the frames back to back.
  * dump=FILE (loop mode): thread 0's first `count` records, in submission
  * order, for the caller's parity check against the oracle.
@@ -48,11 +50,11 @@ static double now_s(void)
 /* ---- options ------------------------------------------------------------- */
 static struct {
 	const char *frames, *mode, *dump;
-	int threads, batch, device, direct;
+	int threads, batch, device, direct, reg;
 	double seconds;
 	uint32_t n, arena;
 	struct ixg_rx_async_cfg acfg;
-} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 2.0, 64, 1u << 16,
+} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 2.0, 64, 1u << 16,
 	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}};
 
 static const uint8_t rss_key[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
@@ -92,7 +94,8 @@ static int load_pool(const char *path)
  * +64 (inc/ix/mbuf.h:73-90) */
 static void **make_arena(uint32_t n, uint8_t **mem)
 {
-	uint8_t *a = aligned_alloc(64, (size_t)n * MBUF_STRIDE);
+	/* (+ the tail bytes the kernels may read past the last frame) */
+	uint8_t *a = aligned_alloc(4096, ((size_t)n * MBUF_STRIDE + IXG_TAIL_PAD + 4095) & ~(size_t)4095);
 	void **p = malloc((size_t)n * sizeof(void *));
 	if (!a || !p)
 		return NULL;
@@ -257,6 +260,11 @@ static int run_loop(void)
 		w->ptrs = make_arena(opt.arena, &w->mem);
 		if (!w->ptrs)
 			return 1;
+		if (opt.reg && (w->rc = ixg_rx_register_memory(w->ctx, w->mem,
+				      ((size_t)opt.arena * MBUF_STRIDE + IXG_TAIL_PAD + 4095) & ~(size_t)4095))) {
+			fprintf(stderr, "register %d: %s\n", i, ixg_strerror(w->rc));
+			return 2;
+		}
 		if (i == 0 && opt.dump)
 			w->dump = malloc(pool_n * sizeof(struct ixg_rx_rec));
 	}
@@ -302,25 +310,28 @@ static int run_loop(void)
 		o += ws[i].nlat;
 	}
 	qsort(lat, nl, sizeof(double), cmp_d);
-	/* host-link bytes per frame of the staged image: frame bytes past the MAC
-	 * addresses (4-aligned) + the length (+ the offset, non-uniform pools) */
+	/* bytes per frame the CPU writes into the staged image: frame bytes past
+	 * the MAC addresses (4-aligned) + the length (+ the offset, non-uniform
+	 * pools); zero copy: the offset and the length only (the kernels read
+	 * the frame in place) */
 	uint64_t staged = 0;
 	int uniform = 1;
 	for (uint32_t i = 0; i < pool_n; i++) {
 		staged += pool_len[i] > 12 ? ((pool_len[i] - 12u + 3u) & ~3u) : 0u;
 		uniform &= pool_len[i] == pool_len[0];
 	}
-	const double h2d = (double)staged / pool_n + 2.0 + (uniform ? 0.0 : 8.0);
+	const double staged_b = opt.reg ? 10.0 : (double)staged / pool_n + 2.0 + (uniform ? 0.0 : 8.0);
 	printf("{\"mode\": \"loop\", \"threads\": %d, \"seconds\": %.3f, \"frames\": %llu, \"mpps\": %.2f, "
 	       "\"iterations\": %llu, \"frames_per_iteration\": %.1f, \"batch\": %d, "
 	       "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"n\": %zu}, "
-	       "\"h2d_bytes_per_frame\": %.1f, \"d2h_bytes_per_frame\": 16, "
-	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d}, "
+	       "\"staged_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
+	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d, "
+	       "\"zero_copy\": %d}, "
 	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}}\n",
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
-	       nl ? lat[nl - 1] : 0.0, nl, h2d, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
-	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, (unsigned long long)st.tcp,
+	       nl ? lat[nl - 1] : 0.0, nl, staged_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
+	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, (unsigned long long)st.tcp,
 	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
 	       (unsigned long long)st.drop);
 	if (opt.dump) {
@@ -441,6 +452,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(k, "cfg_wait_us")) opt.acfg.max_wait_us = (uint32_t)atoi(v);
 		else if (!strcmp(k, "cfg_depth")) opt.acfg.depth = (uint32_t)atoi(v);
 		else if (!strcmp(k, "direct")) opt.acfg.flags = atoi(v) ? IXG_ASYNC_DIRECT : 0;
+		else if (!strcmp(k, "register")) opt.reg = atoi(v);
 		else {
 			fprintf(stderr, "unknown option %s\n", k);
 			return 2;

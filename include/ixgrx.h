@@ -227,6 +227,18 @@ int ixg_rx_poll(void *ctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max, 
 /* Frames submitted and not yet returned by poll, or -errno. */
 int ixg_rx_async_pending(void *ctx);
 
+/* Zero copy: make host memory that holds mbufs (IX's mbuf mempool, its 2 MB
+ * pages, dp/core/mempool.c:198-243) readable by the kernels (page-locked and
+ * mapped, hipHostRegister). With IXG_ASYNC_DIRECT, a submitted frame whose
+ * whole mbuf plus IXG_TAIL_PAD bytes lies inside a registered region is then
+ * not gathered: the kernels read it where it is, over the host link, and the
+ * CPU only stages its pointer and length. Frames outside every region are
+ * gathered as before. Up to 32 regions per context, none overlapping; they
+ * stay registered until ixg_rx_unregister_memory (-EBUSY while frames are
+ * pending) or ixg_rx_fini. 0 or -errno. */
+int ixg_rx_register_memory(void *ctx, void *base, size_t bytes);
+int ixg_rx_unregister_memory(void *ctx, void *base);
+
 /* Host batch from a packed host buffer (same layout rules as
  * ixg_rx_frames, but host pointers). Synchronous. `csum` may be NULL. */
 int ixg_rx_batch_host(void *ctx, const void *frames, const uint64_t *off,

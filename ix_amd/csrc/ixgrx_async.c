@@ -33,6 +33,7 @@ struct ixg_abatch {
 	hipStream_t stream;
 	hipEvent_t done;
 	uint64_t t_open;     /* ns: when its first frame was gathered */
+	uint32_t nabs;       /* frames read in place (registered memory) */
 	uint32_t n, taken;   /* frames held, frames already returned by poll */
 	size_t span;         /* gathered bytes (ixg_gather_mbufs) */
 	uint8_t *h_buf, *d_buf;
@@ -159,7 +160,10 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	if (b->state != AS_OPEN)
 		return 0;
 	struct ixg_stage st;
-	ixg_stage_finish(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
+	if (b->nabs)
+		ixg_stage_finish_abs(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
+	else
+		ixg_stage_finish(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
 	const int direct = (a->cfg.flags & IXG_ASYNC_DIRECT) != 0;
 	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, b->stream);
 	if (rc)
@@ -184,6 +188,7 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
 	b->state = AS_OPEN;
 	b->t_open = t;
 	b->n = b->taken = 0;
+	b->nabs = 0;
 	b->span = 0;
 	a->tail = (a->tail + 1) % a->cfg.depth;
 	a->count++;
@@ -231,8 +236,12 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 			if (step > room)
 				step = (uint32_t)room;
 			const uint32_t take = a->cfg.batch_frames - b->n - m < step ? a->cfg.batch_frames - b->n - m : step;
-			b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, b->h_off + b->n + m,
-						   b->h_len + b->n + m);
+			if (c->nreg && (a->cfg.flags & IXG_ASYNC_DIRECT))
+				b->span = ixg_gather_mbufs_zc(c, b->h_buf, b->span, mbufs + done + m, take,
+							      b->h_off + b->n + m, b->h_len + b->n + m, &b->nabs);
+			else
+				b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, b->h_off + b->n + m,
+							   b->h_len + b->n + m);
 			memcpy(b->mbufs + b->n + m, mbufs + done + m, (size_t)take * sizeof(void *));
 			m += take;
 		}

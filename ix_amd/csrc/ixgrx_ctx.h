@@ -24,6 +24,8 @@ struct ixg_dstate {
 	size_t tail_cap;     /* frames d_tail holds */
 };
 
+#define IXG_MAX_REGIONS 32u
+
 /* one stage of the pipelined host path (ixg_rx_batch_mbufs): pinned
  * staging, device buffers, its own stream and defer state */
 #define IXG_SLOTS 2
@@ -48,6 +50,8 @@ struct ixg_slot {
  * (the skipped MAC bytes), which the launch is told (ixg_kparams.overlap). */
 struct ixg_stage {
 	size_t h2d;          /* bytes to copy */
+	uint64_t base;       /* runs with in-place frames: the address offsets are
+	                        relative to (0: the image itself) */
 	size_t o_off, o_len; /* where the offsets / lengths start in the image */
 	uint32_t stride;     /* fixed-stride run: the stride; else 0 */
 };
@@ -106,6 +110,14 @@ struct ixg_ctx {
 	size_t fdir_cap;             /* slots d_fdir holds (grow-only)*/
 	/* the asynchronous host path (ixgrx_async.c) */
 	struct ixg_async *async;
+	/* host memory registered for in-place reads (ixg_rx_register_memory):
+	 * frames of mbufs inside [lo, hi - IXG_MBUF_STRIDE - IXG_TAIL_PAD] are
+	 * read by the kernels where they are (device address = host + delta) */
+	struct ixg_region {
+		uintptr_t lo, hi;
+		intptr_t delta;
+	} reg[IXG_MAX_REGIONS];
+	uint32_t nreg;
 };
 
 
@@ -133,8 +145,22 @@ IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
  * lengths, returns the staged span (pos of the frame after the last). */
 IXG_INTERNAL size_t ixg_gather_mbufs(uint8_t *frames, size_t pos0, void *const *mbufs, uint32_t n, uint64_t *off, uint16_t *len);
 
+/* The asynchronous path's gather with registered regions (zero copy): a
+ * frame whose mbuf lies in one of c's registered regions is not copied; its
+ * off[k] is its data's device address | IXG_OFF_ABS. Other frames are
+ * gathered as by ixg_gather_mbufs (off[k] = staging position). Returns the
+ * staged span; *nabs counts the in-place frames. */
+#define IXG_OFF_ABS (1ull << 63)
+IXG_INTERNAL size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos, void *const *mbufs,
+				       uint32_t n, uint64_t *off, uint16_t *len, uint32_t *nabs);
+
 IXG_INTERNAL void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint16_t *len, uint32_t n,
 		      struct ixg_stage *st);
+/* the same for a run with in-place frames (ixg_gather_mbufs_zc, nabs > 0):
+ * every offset becomes relative to st->base, the lowest frame address of the
+ * run (staged frames: buf's device address + position) */
+IXG_INTERNAL void ixg_stage_finish_abs(uint8_t *buf, size_t span, uint64_t *off, const uint16_t *len, uint32_t n,
+				      struct ixg_stage *st);
 
 /* enqueue one staged image on `s`: its H2D copy, the kernels, the D2H copy
  * of the records into h_rec; direct: the kernels read the pinned image and

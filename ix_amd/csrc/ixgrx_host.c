@@ -121,6 +121,8 @@ void ixg_rx_fini(void *vctx)
 	if (c->stream)
 		hipStreamSynchronize(c->stream);
 	ixg_async_free(c);
+	for (uint32_t r = 0; r < c->nreg; r++)
+		hipHostUnregister((void *)c->reg[r].lo);
 	for (int k = 0; k < IXG_SLOTS; k++)
 		ixg_slot_free(&c->slot[k]);
 	hipFree(c->d_tab);
@@ -373,6 +375,53 @@ int ixg_rx_set_fdir(void *vctx, const struct ixg_fdir_filter *f, uint32_t n, uin
 	return rc;
 }
 
+/* ---- host memory the kernels read in place (the asynchronous path) ------- */
+
+int ixg_rx_register_memory(void *vctx, void *base, size_t bytes)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !base || bytes < IXG_MBUF_STRIDE + IXG_TAIL_PAD)
+		return -EINVAL;
+	if (c->nreg == IXG_MAX_REGIONS)
+		return -ENOMEM;
+	const uintptr_t lo = (uintptr_t)base, hi = lo + bytes;
+	for (uint32_t r = 0; r < c->nreg; r++)
+		if (lo < c->reg[r].hi && c->reg[r].lo < hi)
+			return -EINVAL; /* overlaps a registered region */
+	HIPCHK(hipSetDevice(c->device));
+	if (hipHostRegister(base, bytes, hipHostRegisterMapped) != hipSuccess)
+		return -EIO;
+	void *dev = NULL;
+	if (hipHostGetDevicePointer(&dev, base, 0) != hipSuccess) {
+		hipHostUnregister(base);
+		return -EIO;
+	}
+	c->reg[c->nreg].lo = lo;
+	c->reg[c->nreg].hi = hi;
+	c->reg[c->nreg].delta = (intptr_t)dev - (intptr_t)lo;
+	c->nreg++;
+	return 0;
+}
+
+int ixg_rx_unregister_memory(void *vctx, void *base)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c)
+		return -EINVAL;
+	for (uint32_t r = 0; r < c->nreg; r++) {
+		if (c->reg[r].lo != (uintptr_t)base)
+			continue;
+		HIPCHK(hipSetDevice(c->device));
+		/* no batch of this context may still read it */
+		if (c->async && ixg_rx_async_pending(c) > 0)
+			return -EBUSY;
+		hipHostUnregister(base);
+		c->reg[r] = c->reg[--c->nreg];
+		return 0;
+	}
+	return -ENOENT;
+}
+
 int ixg_rx_set_split(void *vctx, uint32_t split)
 {
 	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
@@ -504,9 +553,62 @@ size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_
 	return pos;
 }
 
+size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n,
+			   uint64_t *off, uint16_t *len, uint32_t *nabs)
+{
+	uint32_t in_place = 0;
+	for (uint32_t k = 0; k < n; k++) {
+		const uint8_t *mb = (const uint8_t *)mbufs[k];
+		const uintptr_t a = (uintptr_t)mb;
+		size_t l;
+		memcpy(&l, mb, sizeof(l)); /* mbuf->len (inc/ix/mbuf.h:75) */
+		len[k] = (uint16_t)l;
+		uint32_t r = 0;
+		/* the mbuf and the bytes the kernels may read past its frame inside
+		 * the region (ixg_rx_register_memory) */
+		while (r < c->nreg && !(a >= c->reg[r].lo && a + IXG_MBUF_STRIDE + IXG_TAIL_PAD <= c->reg[r].hi))
+			r++;
+		if (r < c->nreg && !(a & 3)) {
+			off[k] = ((uint64_t)(a + IXG_MBUF_HEADER_LEN) + (uint64_t)c->reg[r].delta) | IXG_OFF_ABS;
+			in_place++;
+			continue;
+		}
+		off[k] = pos;
+		if (l > 12) {
+			memcpy(frames + pos + 12, mb + IXG_MBUF_HEADER_LEN + 12, l - 12);
+			pos += (l - 12 + 3) & ~(size_t)3;
+		}
+	}
+	*nabs += in_place;
+	return pos;
+}
+
+void ixg_stage_finish_abs(uint8_t *buf, size_t span, uint64_t *off, const uint16_t *len, uint32_t n,
+			  struct ixg_stage *st)
+{
+	memset(buf + span + 12, 0, IXG_TAIL_PAD + 16);
+	uint64_t lo = ~0ull;
+	for (uint32_t k = 0; k < n; k++) {
+		off[k] = (off[k] & IXG_OFF_ABS) ? (off[k] & ~IXG_OFF_ABS) : (uint64_t)(uintptr_t)buf + off[k];
+		if (off[k] < lo)
+			lo = off[k];
+	}
+	lo &= ~(uint64_t)15;
+	for (uint32_t k = 0; k < n; k++)
+		off[k] -= lo;
+	st->base = lo;
+	st->stride = 0;
+	st->o_off = (span + 12 + IXG_TAIL_PAD + 16 + 7) & ~(size_t)7;
+	memcpy(buf + st->o_off, off, (size_t)n * sizeof(uint64_t));
+	st->o_len = st->o_off + (size_t)n * sizeof(uint64_t);
+	memcpy(buf + st->o_len, len, (size_t)n * sizeof(uint16_t));
+	st->h2d = st->o_len + (size_t)n * sizeof(uint16_t);
+}
+
 void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint16_t *len, uint32_t n,
 		      struct ixg_stage *st)
 {
+	st->base = 0;
 	const size_t last_end = off[n - 1] + (len[n - 1] > 12 ? len[n - 1] : 12);
 	memset(buf + last_end, 0, IXG_TAIL_PAD + 16);
 	int uniform = 1;
@@ -611,9 +713,13 @@ int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_
 	if (direct) {
 		img = h_buf; /* the kernels read the pinned image over the host link */
 	} else {
+		if (st->base)
+			return -EINVAL; /* in-place frames are for kernels on host memory only */
 		HIPCHK(hipMemcpyAsync(d_buf, h_buf, st->h2d, hipMemcpyHostToDevice, s));
 	}
-	int rc = ixg_launch_ds(c, ds, img, st->stride ? NULL : (const uint64_t *)(img + st->o_off),
+	/* frames: the image, or (in-place frames) offsets from st->base */
+	const uint8_t *frames = st->base ? (const uint8_t *)(uintptr_t)st->base : img;
+	int rc = ixg_launch_ds(c, ds, frames, st->stride ? NULL : (const uint64_t *)(img + st->o_off),
 			       (const uint16_t *)(img + st->o_len), st->stride, n, direct ? h_rec : d_rec, NULL, NULL,
 			       st->stride ? 1u : 0u, s);
 	if (rc)

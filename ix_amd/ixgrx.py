@@ -50,6 +50,7 @@ EXPORTS = (
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
     "ixg_ev_batch_dev", "ixg_rx_set_split", "ixg_rx_set_fdir",
     "ixg_rx_async_init", "ixg_rx_submit_mbufs", "ixg_rx_flush", "ixg_rx_poll", "ixg_rx_async_pending",
+    "ixg_rx_register_memory", "ixg_rx_unregister_memory",
 )
 
 # struct ixg_fdir_filter (12 bytes): raw IPs as in the frame, host-order ports
@@ -154,6 +155,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_poll.restype = i32
     lib.ixg_rx_async_pending.argtypes = [vp]
     lib.ixg_rx_async_pending.restype = i32
+    lib.ixg_rx_register_memory.argtypes = [vp, vp, ctypes.c_size_t]
+    lib.ixg_rx_register_memory.restype = i32
+    lib.ixg_rx_unregister_memory.argtypes = [vp, vp]
+    lib.ixg_rx_unregister_memory.restype = i32
     if lib.ixg_abi_version() != ABI_VERSION:
         raise RuntimeError("libixgrx ABI version mismatch")
     _libs[path] = lib
@@ -273,6 +278,13 @@ class RxEngine:
         if rc < 0:
             _check(rc, "ixg_rx_poll", self._lib)
         return mb[:rc], rec[:rc]
+
+    def register_memory(self, base: int, nbytes: int) -> None:
+        """Zero copy: the kernels read frames of mbufs in [base, base+nbytes) in place."""
+        _check(self._lib.ixg_rx_register_memory(self._ctx, base, nbytes), "ixg_rx_register_memory", self._lib)
+
+    def unregister_memory(self, base: int) -> None:
+        _check(self._lib.ixg_rx_unregister_memory(self._ctx, base), "ixg_rx_unregister_memory", self._lib)
 
     def pending(self) -> int:
         rc = self._lib.ixg_rx_async_pending(self._ctx)

@@ -13,7 +13,10 @@
  * runs it. So a host path that read results before synchronizing, or
  * reused a staging buffer whose copy had not run yet, sees wrong records.
  * An RX "launch" runs the oracle's restatement (oracle/ixgrx_oracle.c) over
- * the launch's frames with the configuration fakehip_set_cfg installed.
+ * the launch's frames with the configuration fakehip_set_cfg installed, after
+ * checking that every byte a kernel may read of each frame lies in memory
+ * the device could reach (an allocation of this runtime or a registered
+ * host range): a frame outside them would fault a real GPU, here it aborts.
  */
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
@@ -50,6 +53,41 @@ struct fevent {
 static struct ixg_rx_cfg g_cfg;
 static unsigned long g_launches;
 
+/* memory the device can reach: allocations and registered host ranges */
+#define MAXR 4096
+static struct {
+	uintptr_t lo, hi;
+	int registered;
+} g_mem[MAXR];
+static int g_nmem;
+static unsigned long g_inplace; /* frames read from registered host memory */
+unsigned long fakehip_inplace_frames(void) { return g_inplace; }
+static void mem_add(const void *p, size_t n, int registered)
+{
+	if (g_nmem == MAXR)
+		abort();
+	g_mem[g_nmem].lo = (uintptr_t)p;
+	g_mem[g_nmem].hi = (uintptr_t)p + n;
+	g_mem[g_nmem].registered = registered;
+	g_nmem++;
+}
+static void mem_del(const void *p)
+{
+	for (int i = 0; i < g_nmem; i++)
+		if (g_mem[i].lo == (uintptr_t)p) {
+			g_mem[i] = g_mem[--g_nmem];
+			return;
+		}
+}
+/* 0: unreachable, 1: an allocation, 2: registered host memory */
+static int reachable(uintptr_t lo, uintptr_t hi)
+{
+	for (int i = 0; i < g_nmem; i++)
+		if (lo >= g_mem[i].lo && hi <= g_mem[i].hi)
+			return 1 + g_mem[i].registered;
+	return 0;
+}
+
 void fakehip_set_cfg(const struct ixg_rx_cfg *cfg) { g_cfg = *cfg; }
 unsigned long fakehip_launches(void) { return g_launches; }
 
@@ -63,6 +101,17 @@ static void run_op(struct op *o)
 		memset(o->dst, o->val, o->n);
 		break;
 	case OP_RX: {
+		/* the bytes the kernels may read of frame i: its first max(L, 112)
+		 * bytes and up to 16 past them (IXG_TAIL_PAD covers it) */
+		for (uint32_t i = 0; i < o->p.n; i++) {
+			const uint64_t off = o->p.off ? o->p.off[i] : (uint64_t)i * o->p.stride;
+			const uintptr_t a = (uintptr_t)o->p.base + off;
+			const uint32_t L = o->p.len[i] > 112 ? o->p.len[i] : 112;
+			const int r = reachable(a, a + L + 16);
+			if (!r || !reachable((uintptr_t)(o->p.out + i), (uintptr_t)(o->p.out + i + 1)))
+				abort();
+			g_inplace += r == 2;
+		}
 		struct ixg_rx_cfg c = g_cfg;
 		ixgo_rx_batch(&c, o->p.base, o->p.off, o->p.len, o->p.stride, o->p.n, o->p.out, o->p.csum, 1,
 			      IXGO_HASH_TABLE, IXGO_WORK_FULL);
@@ -132,6 +181,8 @@ hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600 *p, int d)
 hipError_t hipMalloc(void **p, size_t n)
 {
 	*p = aligned_alloc(256, (n + 255) & ~(size_t)255);
+	if (*p)
+		mem_add(*p, n, 0);
 	return *p ? hipSuccess : hipErrorOutOfMemory;
 }
 hipError_t hipHostMalloc(void **p, size_t n, unsigned int f)
@@ -141,11 +192,13 @@ hipError_t hipHostMalloc(void **p, size_t n, unsigned int f)
 }
 hipError_t hipFree(void *p)
 {
+	mem_del(p);
 	free(p);
 	return hipSuccess;
 }
 hipError_t hipHostFree(void *p)
 {
+	mem_del(p);
 	free(p);
 	return hipSuccess;
 }
@@ -243,6 +296,24 @@ hipError_t hipEventQuery(hipEvent_t e)
 		return hipErrorNotReady;
 	}
 	run_to(ev);
+	return hipSuccess;
+}
+
+hipError_t hipHostRegister(void *p, size_t n, unsigned int f)
+{
+	(void)f;
+	mem_add(p, n, 1);
+	return hipSuccess;
+}
+hipError_t hipHostUnregister(void *p)
+{
+	mem_del(p);
+	return hipSuccess;
+}
+hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int f)
+{
+	(void)f;
+	*d = h;
 	return hipSuccess;
 }
 

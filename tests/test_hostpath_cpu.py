@@ -196,3 +196,36 @@ def test_async_rejects_oversized_and_bad_cfg(fake):
                 eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, **bad})
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed"])
+def test_async_zero_copy(fake, kind):
+    """Registered mbuf memory (ixg_rx_register_memory): frames are read in
+    place, nothing of them is gathered; frames of unregistered mbufs in the
+    same batches are gathered; records as the oracle's, in order."""
+    fake.lib.fakehip_inplace_frames.restype = ctypes.c_ulong
+    rng = np.random.default_rng(21)
+    tr, arena, ptrs = _mbufs(kind, 6000, seed=13)
+    tr2, arena2, ptrs2 = _mbufs("imix", 6000, seed=14)  # stays unregistered
+    mix = np.where(rng.random(6000) < 0.7, ptrs, ptrs2)
+    eng = fake()
+    try:
+        eng.async_init(**ixgrx.ASYNC_DEFAULTS)
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        with pytest.raises(RuntimeError, match="ixg_rx_register_memory"):
+            eng.register_memory(arena.ctypes.data + 4096, 1 << 16)  # overlaps
+        n0 = fake.lib.fakehip_inplace_frames()
+        m, r = _loop(eng, ptrs, rng)
+        assert fake.lib.fakehip_inplace_frames() - n0 == len(ptrs)  # every frame read in place
+        assert np.array_equal(m, ptrs)
+        assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+        n1 = fake.lib.fakehip_inplace_frames()
+        m, r = _loop(eng, mix, rng)
+        assert fake.lib.fakehip_inplace_frames() - n1 == int((mix == ptrs).sum())
+        assert np.array_equal(m, mix)
+        assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(mix))
+        eng.unregister_memory(arena.ctypes.data)
+        with pytest.raises(RuntimeError, match="ixg_rx_unregister_memory"):
+            eng.unregister_memory(arena.ctypes.data)
+    finally:
+        eng.close()

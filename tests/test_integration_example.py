@@ -92,7 +92,7 @@ def test_async_loop_builds_and_fails_cleanly_without_gpu(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("extra", [[], ["direct=1"], ["cfg_wait_us=0", "cfg_depth=2"]])
+@pytest.mark.parametrize("extra", [[], ["direct=0"], ["register=1"], ["cfg_wait_us=0", "cfg_depth=2"]])
 def test_async_loop_runs_on_gpu(tmp_path, extra):
     """IX's run loop over the asynchronous path, 4 CPUs (threads), <= 64
     frames per iteration: thread 0's records (submission order) are the
