@@ -346,18 +346,26 @@ struct ixg_listen_key {
 };
 
 /* A snapshot of one context's demux lists (host arrays; ixg_demux_load copies
- * them). Flow groups are the context's local ones: fg_id - dev_idx*512. */
+ * them). Groups are the context's local flow groups (fg_id - dev_idx*512,
+ * g < nfg) followed by n_out outbound groups: the per-CPU groups
+ * ETH_MAX_TOTAL_FG + cpu_id (inc/ix/ethfg.h:135-138) whose active and
+ * TIME-WAIT lists hold the connections the CPU opened (bsys_tcp_connect,
+ * dp/net/tcp_api.c:694), whose frames the flow director steers there
+ * (ixg_rx_set_fdir): group nfg + cpu_id for cpu_id < n_out. */
+#define IXG_MAX_OUTBOUND 1024u
 struct ixg_demux_tables {
-	uint32_t nfg;                       /* flow groups in the snapshot (<= 512) */
+	uint32_t nfg;                       /* local flow groups in the snapshot (<= 512) */
 	uint32_t n_listen;
-	const uint32_t *active_start;       /* nfg*512 + 1 offsets: entries of
+	const uint32_t *active_start;       /* (nfg+n_out)*512 + 1 offsets: entries of
 	                                       fgs[g]->active_tbl[b].pcbs (ethfg.h:83) in
 	                                       list order are active[active_start[g*512+b] ..
 	                                       active_start[g*512+b+1]) */
 	const struct ixg_pcb_key *active;
-	const uint32_t *tw_start;           /* nfg + 1 offsets into tw[]: fgs[g]->tw_pcbs */
+	const uint32_t *tw_start;           /* nfg + n_out + 1 offsets into tw[]: fgs[g]->tw_pcbs */
 	const struct ixg_pcb_key *tw;
 	const struct ixg_listen_key *listen; /* percpu tcp_cpu_lists.listen_pcbs, list order */
+	uint32_t n_out;                     /* outbound groups (CPUs) in the snapshot (<= IXG_MAX_OUTBOUND) */
+	uint32_t rsvd;
 };
 
 /* demux.kind */

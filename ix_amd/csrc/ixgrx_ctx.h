@@ -86,7 +86,7 @@ struct ixg_ctx {
 	size_t d_n_cap;
 	/* PCB demux tables (ixg_demux_load) */
 	int demux_loaded;
-	uint32_t dmx_nfg, dmx_nlisten;
+	uint32_t dmx_nfg, dmx_nout, dmx_nlisten;
 	uint32_t *d_astart, *d_twstart;
 	struct ixg_pcb_key *d_active, *d_tw;
 	struct ixg_listen_key *d_listen;
@@ -130,10 +130,12 @@ struct ixg_ctx {
 /* library-internal functions: not exported from libixgrx.so */
 #define IXG_INTERNAL __attribute__((visibility("hidden")))
 
-/* ixgrx_host.c */
+/* ixgrx_host.c; lflags: IXG_LF_* */
+#define IXG_LF_OVERLAP 1u /* fixed stride, frames overlap the next slot (ixg_kparams.overlap) */
+#define IXG_LF_HOST 2u    /* frames in host memory (ixg_kparams.host_mem) */
 IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
-		  struct ixg_demux_rec *dmx, uint32_t overlap, hipStream_t s);
+		  struct ixg_demux_rec *dmx, uint32_t lflags, hipStream_t s);
 IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
 
 /* The IX-layout gather both host paths use: frames out of mbufs (len =

@@ -27,6 +27,7 @@ struct ixg_dparams {
 	uint32_t n;
 	uint32_t fg_base;             /* dev_idx * 512 */
 	uint32_t nfg;
+	uint32_t n_out;               /* outbound groups after the nfg local ones */
 	uint32_t n_listen;
 	uint32_t rsvd;
 };

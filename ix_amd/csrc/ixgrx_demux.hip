@@ -17,6 +17,7 @@
 
 #include "../../include/ixgrx.h"
 #include "ixgrx_demux.h"
+#include "ixgrx_internal.h"
 #include "ixgrx_walk.h"
 
 #define DEV __device__ __forceinline__
@@ -65,7 +66,7 @@ DEV void walk_item(const DParams& p, uint32_t i, const Item& it) {
   const uint32_t verdict = (it.rec.x >> 16) & 0xffu;
   uint32_t kind = IXG_D_NONE, id = 0;
   if (verdict == IXG_V_TCP) {
-    const uint32_t fg = (it.rec.x & 0xffffu) - p.fg_base;  // ethfg: fgs[pkt->fg_id]
+    const uint32_t fg = ixg_demux_group(it.rec.x & 0xffffu, p.fg_base, p.nfg, p.n_out);  // fgs[pkt->fg_id]
     const uint32_t bucket = it.rec.w & 0xffffu;             // tcp_to_idx (tcp_in.c:233)
     const uint32_t tflags = (it.rec.w >> 16) & 0xffu;
     const uint32_t ihl = (it.h0.x >> 16) & 15u;             // frame byte 14
@@ -83,7 +84,7 @@ DEV void walk_item(const DParams& p, uint32_t i, const Item& it) {
       dw = v.y & 0xffffu;
     }
     const uint32_t sport = bswap16(sw), dport = bswap16(dw);  // tcp_in.c:230-231
-    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
+    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
     ixgwalk::walk(t, fg, bucket, tflags, src, dst, sport | (dport << 16), id, kind);
   }
   const u32x2 o = {id, kind};

@@ -276,7 +276,8 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 	p.fg_mask = (uint32_t)c->cfg.nb_rx_fgs - 1u;
 	p.zero = c->d_zero;
 	p.fdir = c->d_fdir;
-	p.overlap = overlap;
+	p.overlap = overlap & 1u;
+	p.host_mem = (overlap >> 1) & 1u;
 	if (dmx) {
 		p.dmx = dmx;
 		p.active_start = c->d_astart;
@@ -286,6 +287,7 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		p.tw = c->d_tw;
 		p.listen = c->d_listen;
 		p.nfg = c->dmx_nfg;
+		p.n_out = c->dmx_nout;
 		p.n_listen = c->dmx_nlisten;
 	}
 	size_t nchunks = ((size_t)n + 63) / 64;
@@ -721,7 +723,7 @@ int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_
 	const uint8_t *frames = st->base ? (const uint8_t *)(uintptr_t)st->base : img;
 	int rc = ixg_launch_ds(c, ds, frames, st->stride ? NULL : (const uint64_t *)(img + st->o_off),
 			       (const uint16_t *)(img + st->o_len), st->stride, n, direct ? h_rec : d_rec, NULL, NULL,
-			       st->stride ? 1u : 0u, s);
+			       (st->stride ? IXG_LF_OVERLAP : 0u) | (direct ? IXG_LF_HOST : 0u), s);
 	if (rc)
 		return rc;
 	if (!direct)
@@ -845,12 +847,13 @@ static int csr_ok(const uint32_t *start, size_t rows)
 int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
 {
 	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
-	if (!c || !t || t->nfg > IXG_ETH_MAX_NUM_FG)
+	if (!c || !t || t->nfg > IXG_ETH_MAX_NUM_FG || t->n_out > IXG_MAX_OUTBOUND)
 		return -EINVAL;
-	const size_t na_rows = (size_t)t->nfg * IXG_PCB_BUCKETS;
-	if (!csr_ok(t->active_start, na_rows) || !csr_ok(t->tw_start, t->nfg))
+	const size_t ng = (size_t)t->nfg + t->n_out; /* local groups, then outbound */
+	const size_t na_rows = ng * IXG_PCB_BUCKETS;
+	if (!csr_ok(t->active_start, na_rows) || !csr_ok(t->tw_start, ng))
 		return -EINVAL;
-	const size_t na = t->active_start[na_rows], ntw = t->tw_start[t->nfg];
+	const size_t na = t->active_start[na_rows], ntw = t->tw_start[ng];
 	if ((na && !t->active) || (ntw && !t->tw) || (t->n_listen && !t->listen))
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
@@ -858,7 +861,7 @@ int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
 	c->demux_loaded = 0;
 	int rc;
 	if ((rc = upload((void **)&c->d_astart, t->active_start, (na_rows + 1) * sizeof(uint32_t))) ||
-	    (rc = upload((void **)&c->d_twstart, t->tw_start, ((size_t)t->nfg + 1) * sizeof(uint32_t))) ||
+	    (rc = upload((void **)&c->d_twstart, t->tw_start, (ng + 1) * sizeof(uint32_t))) ||
 	    (rc = upload((void **)&c->d_active, t->active, na * sizeof(struct ixg_pcb_key))) ||
 	    (rc = upload((void **)&c->d_tw, t->tw, ntw * sizeof(struct ixg_pcb_key))) ||
 	    (rc = upload((void **)&c->d_listen, t->listen, (size_t)t->n_listen * sizeof(struct ixg_listen_key))))
@@ -881,6 +884,7 @@ int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
 	if (rc)
 		return rc;
 	c->dmx_nfg = t->nfg;
+	c->dmx_nout = t->n_out;
 	c->dmx_nlisten = t->n_listen;
 	c->demux_loaded = 1;
 	return 0;
@@ -905,6 +909,7 @@ static int demux_launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *
 	p.n = n;
 	p.fg_base = (uint32_t)c->cfg.dev_idx * IXG_ETH_MAX_NUM_FG;
 	p.nfg = c->dmx_nfg;
+	p.n_out = c->dmx_nout;
 	p.n_listen = c->dmx_nlisten;
 	return ixgrx_demux_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
 }

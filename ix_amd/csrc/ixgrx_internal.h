@@ -64,7 +64,8 @@ struct ixg_kparams {
 	const uint32_t *tw_start;
 	const struct ixg_pcb_key *tw;
 	const struct ixg_listen_key *listen;
-	uint32_t nfg;
+	uint32_t nfg;          /* the snapshot's local flow groups */
+	uint32_t n_out;        /* ... and its outbound groups, after them (ixg_demux_group) */
 	uint32_t n_listen;
 	const uint8_t *zero;   /* IXG_ZERO_PAGE zero bytes: stand-in source for
 	                          loads that must read nothing */
@@ -74,6 +75,10 @@ struct ixg_kparams {
 	 * order), 1 = used}: open addressing, slot = ixg_fdir_hash(...) & mask,
 	 * linear probing */
 	const uint32_t *fdir;
+	uint32_t host_mem;     /* the frames are in host memory (the asynchronous path's
+	                          DIRECT mode): every load crosses the host link, so
+	                          the span-staged short kernel runs one wave per chunk
+	                          (latency-bound) instead of one per 64 chunks */
 	uint32_t overlap;      /* fixed-stride batches: frames may run up to 64 bytes
 	                          past their slot (the host paths' staging, whose
 	                          skipped MAC bytes overlap the previous frame) */
@@ -96,6 +101,20 @@ IXG_HD static inline uint32_t ixg_fdir_hash(uint32_t src, uint32_t dst, uint32_t
 	return h ^ (h >> 15) ^ (h >> 27);
 }
 typedef struct ixg_kparams ixg_kparams;
+
+/* The demux snapshot's group of a record's fg_id (struct ixg_demux_tables):
+ * a local flow group (fg_id - dev_idx*512 < nfg), or the outbound group of
+ * CPU fg_id - IXG_ETH_MAX_TOTAL_FG (< n_out), stored after the local ones
+ * (eth_input's cur_fg = fgs[pkt->fg_id], dp/net/ip.c:125, for a frame the
+ * flow director steered, ethfg.c:502-505); IXG_NO_GROUP when the snapshot
+ * has no such group (the lookup then goes straight to the listen list). */
+#define IXG_NO_GROUP 0xfffffffeu
+IXG_HD static inline uint32_t ixg_demux_group(uint32_t fg_id, uint32_t fg_base, uint32_t nfg, uint32_t n_out)
+{
+	if (fg_id >= IXG_ETH_MAX_TOTAL_FG)
+		return fg_id - IXG_ETH_MAX_TOTAL_FG < n_out ? nfg + (fg_id - IXG_ETH_MAX_TOTAL_FG) : IXG_NO_GROUP;
+	return fg_id - fg_base < nfg ? fg_id - fg_base : IXG_NO_GROUP;
+}
 
 #define IXG_ZERO_PAGE 4096u
 #define IXG_PRESENT_WORDS 8u

@@ -635,8 +635,9 @@ DEV void store_demux(const KParams& p, uint32_t i, const Rec& r, uint32_t src, u
   if (!DMX || !p.dmx) return;
   uint32_t id = 0, kind = IXG_D_NONE;
   if (((r.w0 >> 16) & 0xffu) == IXG_V_TCP) {
-    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
-    ixgwalk::walk(t, (r.w0 & 0xffffu) - p.fg_base, r.w3 & 0xffffu, (r.w3 >> 16) & 0xffu, src, dst, ports, id, kind);
+    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
+    ixgwalk::walk(t, ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out), r.w3 & 0xffffu, (r.w3 >> 16) & 0xffu,
+                  src, dst, ports, id, kind);
   }
   typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
   reinterpret_cast<u32x2v*>(p.dmx)[i] = u32x2v{id, kind};
@@ -1557,7 +1558,7 @@ struct PendDmx {
 constexpr uint32_t kNoDmx = 0xffffffffu;
 
 DEV ixgwalk::Tables dmx_tables(const KParams& p) {
-  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg, p.n_listen};
+  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
 }
 
 // record r of frame i (valid lanes) -> pending lookup, line loads issued
@@ -1565,7 +1566,7 @@ DEV void dmx_issue(const KParams& p, bool valid, uint32_t i, const Rec& r, uint3
                    int lane, PendDmx& q) {
   const bool tcp = valid && ((r.w0 >> 16) & 0xffu) == IXG_V_TCP;
   q.i = valid ? i : kNoDmx;
-  q.fg = tcp ? (r.w0 & 0xffffu) - p.fg_base : kNoDmx;
+  q.fg = tcp ? ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out) : kNoDmx;
   q.tflags = (r.w3 >> 16) & 0xffu;
   q.src = src;
   q.dst = dst;
@@ -3133,7 +3134,7 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     // the general kernels: one wave per 64 chunks; the compacted A/B build:
     // one block per 64 chunks per wave
     const uint64_t ngroups = (nchunks + 63u) / 64u, bw = (uint64_t)ks.block / 64u;
-    const uint64_t want = (ngroups + bw - 1) / bw;
+    const uint64_t want = ((p.host_mem ? nchunks : ngroups) + bw - 1) / bw;
     KParams ps = p;
     ps.self_sample = self ? 1u : 0u;
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,

@@ -24,7 +24,8 @@ struct Tables {
   const uint32_t* tw_start;      // nfg + 1
   const ixg_pcb_key* tw;
   const ixg_listen_key* listen;
-  uint32_t nfg, n_listen;
+  uint32_t nfg;  // groups in the snapshot: local, then outbound (ixg_demux_group)
+  uint32_t n_listen;
 };
 
 // tcp_input_find_list (tcp_in.c:122-143): the first entry of [s, e) whose
@@ -41,7 +42,7 @@ __device__ __forceinline__ bool find_list(const ixg_pcb_key* __restrict__ ent, u
   return false;
 }
 
-// The 64-byte bucket line of local flow group `fg`, PCB bucket `bucket`
+// The 64-byte bucket line of the snapshot's group `fg` (ixg_demux_group), PCB bucket `bucket`
 // (null when fg is not a group of the tables)
 __device__ __forceinline__ const u32x4* bucket_line(const Tables& t, uint32_t fg, uint32_t bucket) {
   return fg < t.nfg ? reinterpret_cast<const u32x4*>(t.bline) + 4u * (fg * IXG_PCB_BUCKETS + bucket) : nullptr;

@@ -37,7 +37,7 @@ EXPORTS = ("ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg
 class _Tables(ctypes.Structure):
     _fields_ = [("nfg", ctypes.c_uint32), ("n_listen", ctypes.c_uint32), ("active_start", ctypes.c_void_p),
                 ("active", ctypes.c_void_p), ("tw_start", ctypes.c_void_p), ("tw", ctypes.c_void_p),
-                ("listen", ctypes.c_void_p)]
+                ("listen", ctypes.c_void_p), ("n_out", ctypes.c_uint32), ("rsvd", ctypes.c_uint32)]
 
 
 def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
@@ -81,50 +81,71 @@ def flow_of(cfg: ixgrx.Config, remote_ip, local_ip, remote_port, local_port):
 
 @dataclass
 class DemuxTables:
-    """A CSR snapshot of one context's demux lists (struct ixg_demux_tables)."""
+    """A CSR snapshot of one context's demux lists (struct ixg_demux_tables):
+    nfg local flow groups, then n_out outbound groups (one per CPU: group
+    nfg + cpu_id holds the connections whose frames the flow director steers
+    to outbound flow group ETH_MAX_TOTAL_FG + cpu_id)."""
     nfg: int
-    active_start: np.ndarray  # u32, nfg*512 + 1
+    active_start: np.ndarray  # u32, (nfg+n_out)*512 + 1
     active: np.ndarray        # PCB_DTYPE
-    tw_start: np.ndarray      # u32, nfg + 1
+    tw_start: np.ndarray      # u32, nfg + n_out + 1
     tw: np.ndarray            # PCB_DTYPE
     listen: np.ndarray        # LISTEN_DTYPE
+    n_out: int = 0
 
     @classmethod
     def from_lists(cls, nfg: int, active_fg, active_bucket, active: np.ndarray, tw_fg, tw: np.ndarray,
-                   listen: np.ndarray) -> "DemuxTables":
-        """Lists given flat, in list order, with each entry's flow group
-        (and bucket for active PCBs); a stable sort keeps list order inside
-        every (fg, bucket) list."""
+                   listen: np.ndarray, n_out: int = 0) -> "DemuxTables":
+        """Lists given flat, in list order, with each entry's group (a local
+        flow group < nfg, or nfg + cpu_id for an outbound group) and bucket
+        for active PCBs; a stable sort keeps list order inside every
+        (group, bucket) list."""
         active = np.ascontiguousarray(active, dtype=PCB_DTYPE)
         tw = np.ascontiguousarray(tw, dtype=PCB_DTYPE)
+        ng = nfg + n_out
         afg = np.asarray(active_fg, dtype=np.int64)
         abk = np.asarray(active_bucket, dtype=np.int64)
         tfg = np.asarray(tw_fg, dtype=np.int64)
-        if (afg >= nfg).any() or (tfg >= nfg).any() or (abk >= BUCKETS).any():
+        if (afg >= ng).any() or (tfg >= ng).any() or (abk >= BUCKETS).any():
             raise ValueError("flow group or bucket out of range")
         row = afg * BUCKETS + abk
         order = np.argsort(row, kind="stable")
-        astart = np.zeros(nfg * BUCKETS + 1, dtype=np.uint32)
-        astart[1:] = np.cumsum(np.bincount(row, minlength=nfg * BUCKETS)[:nfg * BUCKETS])
+        astart = np.zeros(ng * BUCKETS + 1, dtype=np.uint32)
+        astart[1:] = np.cumsum(np.bincount(row, minlength=ng * BUCKETS)[:ng * BUCKETS])
         torder = np.argsort(tfg, kind="stable")
-        tstart = np.zeros(nfg + 1, dtype=np.uint32)
-        tstart[1:] = np.cumsum(np.bincount(tfg, minlength=nfg)[:nfg])
+        tstart = np.zeros(ng + 1, dtype=np.uint32)
+        tstart[1:] = np.cumsum(np.bincount(tfg, minlength=ng)[:ng])
         return cls(nfg, astart, active[order].copy(), tstart, tw[torder].copy(),
-                   np.ascontiguousarray(listen, dtype=LISTEN_DTYPE))
+                   np.ascontiguousarray(listen, dtype=LISTEN_DTYPE), n_out)
 
     @classmethod
-    def build(cls, cfg: ixgrx.Config, active: np.ndarray, tw: np.ndarray, listen: np.ndarray) -> "DemuxTables":
-        """Place each PCB in the flow group and bucket its packets hash to."""
+    def build(cls, cfg: ixgrx.Config, active: np.ndarray, tw: np.ndarray, listen: np.ndarray,
+              outbound=None, n_out: int = 0) -> "DemuxTables":
+        """Place each PCB in the flow group and bucket its packets hash to.
+        outbound: (active, tw, cpu of each active, cpu of each tw) of the
+        CPUs' outbound connections, placed in group nfg + cpu (their bucket
+        is tcp_to_idx all the same); n_out: outbound groups (CPUs)."""
         active = np.ascontiguousarray(active, dtype=PCB_DTYPE)
         tw = np.ascontiguousarray(tw, dtype=PCB_DTYPE)
         afg, abk = flow_of(cfg, active["remote_ip"], active["local_ip"], active["remote_port"],
                            active["local_port"])
         tfg, _ = flow_of(cfg, tw["remote_ip"], tw["local_ip"], tw["remote_port"], tw["local_port"])
-        return cls.from_lists(cfg.nb_rx_fgs, afg, abk, active, tfg, tw, listen)
+        if outbound is not None:
+            oa, ot, oac, otc = outbound
+            oa = np.ascontiguousarray(oa, dtype=PCB_DTYPE)
+            ot = np.ascontiguousarray(ot, dtype=PCB_DTYPE)
+            _, obk = flow_of(cfg, oa["remote_ip"], oa["local_ip"], oa["remote_port"], oa["local_port"])
+            active = np.concatenate([active, oa])
+            afg = np.concatenate([afg, cfg.nb_rx_fgs + np.asarray(oac, np.uint32)])
+            abk = np.concatenate([abk, obk])
+            tw = np.concatenate([tw, ot])
+            tfg = np.concatenate([tfg, cfg.nb_rx_fgs + np.asarray(otc, np.uint32)])
+        return cls.from_lists(cfg.nb_rx_fgs, afg, abk, active, tfg, tw, listen, n_out)
 
     def to_c(self) -> _Tables:
         t = _Tables()
         t.nfg = self.nfg
+        t.n_out = self.n_out
         t.n_listen = len(self.listen)
         t.active_start = self.active_start.ctypes.data
         t.active = self.active.ctypes.data if len(self.active) else None

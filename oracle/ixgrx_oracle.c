@@ -680,8 +680,15 @@ void ixgo_demux_one(const struct ixg_demux_tables *t, uint32_t fg_base, const ui
 	uint32_t ihl = B(&f, 14) & 15u, l4 = 14 + 4 * ihl;
 	uint32_t src = Braw32(&f, 26), dst = Braw32(&f, 30);
 	uint16_t sport = B16(&f, l4), dport = B16(&f, l4 + 2); /* ntohs, tcp_in.c:230-231 */
-	uint32_t fg = (uint32_t)rec->fg_id - fg_base;            /* cur_fg = fgs[pkt->fg_id], ip.c:125 */
-	if (fg < t->nfg) {
+	/* cur_fg = fgs[pkt->fg_id] (ip.c:125): a local flow group, or for a frame
+	 * the flow director steered, the CPU's outbound group ETH_MAX_TOTAL_FG +
+	 * cpu_id (ethfg.c:502-505), stored after the local ones */
+	uint32_t fg;
+	if (rec->fg_id >= IXG_ETH_MAX_TOTAL_FG)
+		fg = rec->fg_id - IXG_ETH_MAX_TOTAL_FG < t->n_out ? t->nfg + (rec->fg_id - IXG_ETH_MAX_TOTAL_FG) : ~0u;
+	else
+		fg = (uint32_t)rec->fg_id - fg_base < t->nfg ? (uint32_t)rec->fg_id - fg_base : ~0u;
+	if (fg != ~0u) {
 		/* active_tbl[idx] with idx = tcp_to_idx (tcp_in.c:233,249) */
 		uint32_t a = fg * IXG_PCB_BUCKETS + rec->pcb_bucket;
 		const struct ixg_pcb_key *pcb =

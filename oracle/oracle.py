@@ -184,11 +184,11 @@ def ref_bench(tr, key: bytes, mode: str, procs: int, seconds: float, mbufs_per_p
 class _DemuxTables(ctypes.Structure):
     _fields_ = [("nfg", ctypes.c_uint32), ("n_listen", ctypes.c_uint32), ("active_start", ctypes.c_void_p),
                 ("active", ctypes.c_void_p), ("tw_start", ctypes.c_void_p), ("tw", ctypes.c_void_p),
-                ("listen", ctypes.c_void_p)]
+                ("listen", ctypes.c_void_p), ("n_out", ctypes.c_uint32), ("rsvd", ctypes.c_uint32)]
 
 
 def demux_batch(nfg: int, active_start, active, tw_start, tw, listen, fg_base: int, blob: np.ndarray, off,
-                lens: np.ndarray, stride: int, rec: np.ndarray) -> np.ndarray:
+                lens: np.ndarray, stride: int, rec: np.ndarray, n_out: int = 0) -> np.ndarray:
     """ixgo_demux_batch (tcp_in.c:233-323, 500-510) over the CSR lists;
     returns the 8-byte demux records as an (n, 8) u8 array."""
     L = lib()
@@ -200,6 +200,7 @@ def demux_batch(nfg: int, active_start, active, tw_start, tw, listen, fg_base: i
     arrs = [np.ascontiguousarray(a) for a in (active_start, active, tw_start, tw, listen)]
     t = _DemuxTables()
     t.nfg = nfg
+    t.n_out = n_out
     t.n_listen = len(arrs[4])
     t.active_start, t.active, t.tw_start, t.tw, t.listen = [a.ctypes.data if a.size else None for a in arrs]
     n = int(lens.shape[0])

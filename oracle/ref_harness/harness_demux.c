@@ -16,9 +16,14 @@
  *   - [RST] the no-PCB outcome (:500-510) is restated: RST unless the
  *     segment carries TCP_RST.
  *
- * Input (LE): "IXGDMXIN", u32 n, u32 fg_base, u32 nfg, u32 n_listen,
- *   u32 n_active, u32 n_tw, u32 active_start[nfg*512+1],
- *   struct ixg_pcb_key active[n_active], u32 tw_start[nfg+1],
+ * Groups: fgs[pkt->fg_id] (dp/net/ip.c:125) is restated as an index into the
+ * file's lists: a local flow group fg_id - fg_base < nfg, or an outbound
+ * group ETH_MAX_TOTAL_FG + cpu (cpu < n_out; the flow director's frames,
+ * ethfg.c:502-505) at index nfg + cpu.
+ *
+ * Input (LE): "IXGDMXI2", u32 n, u32 fg_base, u32 nfg, u32 n_out, u32 n_listen,
+ *   u32 n_active, u32 n_tw, u32 active_start[(nfg+n_out)*512+1],
+ *   struct ixg_pcb_key active[n_active], u32 tw_start[nfg+n_out+1],
  *   struct ixg_pcb_key tw[n_tw], struct ixg_listen_key listen[n_listen],
  *   u16 len[n], u32 off[n], u32 blob_len, blob, struct ixg_rx_rec rec[n].
  * Output (LE): "IXGDMXOT", u32 n, struct ixg_demux_rec[n].
@@ -76,13 +81,14 @@ int main(int argc, char **argv)
 	if (!fi)
 		die("open input");
 	char magic[8];
-	uint32_t h[6];
-	if (fread(magic, 1, 8, fi) != 8 || memcmp(magic, "IXGDMXIN", 8) || fread(h, 4, 6, fi) != 6)
+	uint32_t h[7];
+	if (fread(magic, 1, 8, fi) != 8 || memcmp(magic, "IXGDMXI2", 8) || fread(h, 4, 7, fi) != 7)
 		die("bad header");
-	uint32_t n = h[0], fg_base = h[1], nfg = h[2], nl = h[3], na = h[4], ntw = h[5];
-	uint32_t *astart = rd(fi, ((size_t)nfg * IXG_PCB_BUCKETS + 1) * 4);
+	uint32_t n = h[0], fg_base = h[1], nfg = h[2], nout = h[3], nl = h[4], na = h[5], ntw = h[6];
+	const size_t ng = (size_t)nfg + nout;
+	uint32_t *astart = rd(fi, (ng * IXG_PCB_BUCKETS + 1) * 4);
 	struct ixg_pcb_key *act = rd(fi, (size_t)na * sizeof(*act));
-	uint32_t *twstart = rd(fi, ((size_t)nfg + 1) * 4);
+	uint32_t *twstart = rd(fi, (ng + 1) * 4);
 	struct ixg_pcb_key *tw = rd(fi, (size_t)ntw * sizeof(*tw));
 	struct ixg_listen_key *lis = rd(fi, (size_t)nl * sizeof(*lis));
 	uint16_t *len = rd(fi, (size_t)n * 2);
@@ -106,8 +112,9 @@ int main(int argc, char **argv)
 			die("TCP record on a frame without ports");
 		uint32_t src = raw32(f + 26), dst = raw32(f + 30);
 		uint16_t sport = (uint16_t)((f[l4] << 8) | f[l4 + 1]), dport = (uint16_t)((f[l4 + 2] << 8) | f[l4 + 3]);
-		uint32_t fg = (uint32_t)r->fg_id - fg_base;
-		if (fg < nfg) {
+		uint32_t fg = r->fg_id >= IXG_ETH_MAX_TOTAL_FG ? nfg + (r->fg_id - IXG_ETH_MAX_TOTAL_FG)
+							    : (uint32_t)r->fg_id - fg_base;
+		if (r->fg_id >= IXG_ETH_MAX_TOTAL_FG ? r->fg_id - IXG_ETH_MAX_TOTAL_FG < nout : fg < nfg) {
 			uint32_t a = fg * IXG_PCB_BUCKETS + r->pcb_bucket;
 			uint32_t s = astart[a], e = astart[a + 1];
 			int k = ref_find_list(to_ref(act, s, e), (int)(e - s), src, dst, sport, dport);

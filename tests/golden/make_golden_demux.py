@@ -40,13 +40,13 @@ BUCKETS = 512
 TCP = 0x01
 
 
-def run_demux(frames, rec, fg_base, nfg, astart, active, tstart, tw, listen):
+def run_demux(frames, rec, fg_base, nfg, astart, active, tstart, tw, listen, n_out=0):
     tr = traces.pack(frames)
     with tempfile.TemporaryDirectory() as td:
         fi, fo = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
         with open(fi, "wb") as f:
-            f.write(b"IXGDMXIN")
-            f.write(struct.pack("<6I", len(frames), fg_base, nfg, len(listen), len(active), len(tw)))
+            f.write(b"IXGDMXI2")
+            f.write(struct.pack("<7I", len(frames), fg_base, nfg, n_out, len(listen), len(active), len(tw)))
             for a in (astart, active, tstart, tw, listen):
                 f.write(np.ascontiguousarray(a).tobytes())
             f.write(tr.len.astype(np.uint16).tobytes())
@@ -66,7 +66,7 @@ def ip(b: bytes) -> int:
     return int(np.frombuffer(b, "<u4")[0])
 
 
-def frames_and_records(rng, key, nb, dev):
+def frames_and_records(rng, key, nb, dev, fdir_frac=0.0, cpu=0):
     fr = [bytes(r) for r in traces.build_ipv4(rng, 400, 60, 6)]
     for ihl in range(6, 16):  # ports behind IP options
         fr += [bytes(r) for r in traces.build_ipv4(rng, 3, 120, 6, ihl=ihl)]
@@ -81,11 +81,16 @@ def frames_and_records(rng, key, nb, dev):
                        dst=bytes(rng.integers(0, 256, 4, dtype=np.uint8)), tcp_flags=(0x04, 0x14, 0x11, 0x3f)[k % 4]))
     fr += [ipv4(proto=17), ipv4(proto=1, icmp_type=8, payload=b"ping"), ipv4(ethertype=0x0806),
            ipv4(fix_l4=False, payload=b"bad"), ipv4(proto=6, doff_field=15), ipv4(proto=6)[:40]]
-    rec, _ = run_ref(fr, key, nb, dev, 0)
-    return fr, rec
+    filt = None
+    if fdir_frac:  # flow-director filters on a share of the TCP tuples (outbound connections)
+        from make_golden import fdir_filter
+        tcp = [f for f in fr if len(f) >= 38 and f[12:14] == b"\x08\x00" and f[23] == 6]
+        filt = [fdir_filter(f) for f in tcp if rng.random() < fdir_frac]
+    rec, _ = run_ref(fr, key, nb, dev, 0, filt, cpu)
+    return fr, rec, filt
 
 
-def tables(rng, fr, rec, nfg, fg_base, with_listen):
+def tables(rng, fr, rec, nfg, fg_base, with_listen, n_out=0):
     tr = traces.pack(fr)
     tcp = np.nonzero(rec[:, 2] == TCP)[0]
     act_rows, act_keys, tw_fg, tw_keys = [], [], [], []
@@ -100,9 +105,10 @@ def tables(rng, fr, rec, nfg, fg_base, with_listen):
         nid[0] += 1
         return nid[0]
 
+    ng = nfg + n_out
     for i in tcp:
         fg = int(rec[i, 0]) | (int(rec[i, 1]) << 8)
-        g = fg - fg_base
+        g = fg - fg_base if fg < 8192 else nfg + (fg - 8192)  # fgs[fg_id]: local, or outbound after them
         b = int(rec[i, 12]) | (int(rec[i, 13]) << 8)
         u = rng.random()
         rk = key_of(i, new_id())
@@ -124,29 +130,29 @@ def tables(rng, fr, rec, nfg, fg_base, with_listen):
         elif u < 0.7:  # right tuple, wrong bucket
             act_rows.append((g, (b + 1) % BUCKETS)), act_keys.append(rk)
     for _ in range(300):  # unrelated connections
-        act_rows.append((int(rng.integers(0, 128)), int(rng.integers(0, BUCKETS))))
+        act_rows.append((int(rng.integers(0, max(128, ng))), int(rng.integers(0, BUCKETS))))
         act_keys.append((int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32)), int(rng.integers(0, 65536)),
                          int(rng.integers(0, 65536)), new_id()))
     for _ in range(40):
-        tw_fg.append(int(rng.integers(0, 128)))
+        tw_fg.append(int(rng.integers(0, max(128, ng))))
         tw_keys.append((int(rng.integers(0, 2**32)), int(rng.integers(0, 2**32)), int(rng.integers(0, 65536)),
                         int(rng.integers(0, 65536)), new_id()))
-    keep = [k for k, (g, _) in enumerate(act_rows) if g < nfg]
+    keep = [k for k, (g, _) in enumerate(act_rows) if 0 <= g < ng]
     act_rows = [act_rows[k] for k in keep]
     act_keys = [act_keys[k] for k in keep]
-    tkeep = [k for k, g in enumerate(tw_fg) if g < nfg]
+    tkeep = [k for k, g in enumerate(tw_fg) if 0 <= g < ng]
     tw_fg = [tw_fg[k] for k in tkeep]
     tw_keys = [tw_keys[k] for k in tkeep]
     row = np.array([g * BUCKETS + b for g, b in act_rows], dtype=np.int64)
     order = np.argsort(row, kind="stable")
     active = np.array(act_keys, dtype=PCB)[order]
-    astart = np.zeros(nfg * BUCKETS + 1, dtype=np.uint32)
-    astart[1:] = np.cumsum(np.bincount(row, minlength=nfg * BUCKETS))
+    astart = np.zeros(ng * BUCKETS + 1, dtype=np.uint32)
+    astart[1:] = np.cumsum(np.bincount(row, minlength=ng * BUCKETS))
     tfg = np.array(tw_fg, dtype=np.int64)
     torder = np.argsort(tfg, kind="stable")
     tw = np.array(tw_keys, dtype=PCB)[torder]
-    tstart = np.zeros(nfg + 1, dtype=np.uint32)
-    tstart[1:] = np.cumsum(np.bincount(tfg, minlength=nfg))
+    tstart = np.zeros(ng + 1, dtype=np.uint32)
+    tstart[1:] = np.cumsum(np.bincount(tfg, minlength=ng))
     listen = np.zeros(0, dtype=LISTEN)
     if with_listen:
         listen = np.array([(ip(b"\x0a\x00\x00\x03"), 80, 0, 1, 0), (0, 8080, 0, 2, 0), (ip(b"\x0a\x00\x00\x02"), 80, 0, 3, 0),
@@ -155,15 +161,17 @@ def tables(rng, fr, rec, nfg, fg_base, with_listen):
     return astart, active, tstart, tw, listen
 
 
-def save(name, rng, key, nb, dev, nfg, with_listen, note):
-    fr, rec = frames_and_records(rng, key, nb, dev)
+def save(name, rng, key, nb, dev, nfg, with_listen, note, n_out=0, fdir_frac=0.0, cpu=0):
+    fr, rec, filt = frames_and_records(rng, key, nb, dev, fdir_frac, cpu)
     fg_base = dev * 512
-    astart, active, tstart, tw, listen = tables(rng, fr, rec, nfg, fg_base, with_listen)
-    dmx, tr = run_demux(fr, rec, fg_base, nfg, astart, active, tstart, tw, listen)
+    astart, active, tstart, tw, listen = tables(rng, fr, rec, nfg, fg_base, with_listen, n_out)
+    dmx, tr = run_demux(fr, rec, fg_base, nfg, astart, active, tstart, tw, listen, n_out)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), blob=tr.blob, off=tr.off, len=tr.len,
                         key=np.frombuffer(key, np.uint8), nb_rx_fgs=np.uint16(nb), dev_idx=np.uint16(dev),
                         rec=rec, nfg=np.uint32(nfg), active_start=astart, active=active, tw_start=tstart, tw=tw,
-                        listen=listen, demux=dmx, note=np.array(note))
+                        listen=listen, demux=dmx, note=np.array(note), n_out=np.uint32(n_out),
+                        **({"fdir": np.frombuffer(b"".join(filt), np.uint8).reshape(-1, 12),
+                            "fdir_cpu": np.uint16(cpu)} if filt else {}))
     kinds = dmx[:, 4]
     print(f"{name}: {len(fr)} frames, {len(active)} active, {len(tw)} tw, {len(listen)} listen, "
           f"kinds {dict(zip(*np.unique(kinds, return_counts=True)))}")
@@ -177,6 +185,9 @@ def main():
          "MS key, 128 groups, dev_idx 2; listen list (exact, ANY, last-entry quirk)")
     save("demux_nolisten_nfg64", rng, traces.RSS_KEY, 128, 0, 64, False,
          "no listen list (RESET / DROP), tables for local groups 0..63 only")
+    save("demux_fdir_outbound", rng, traces.RSS_KEY, 128, 1, 128, True,
+         "flow-director filters on ~40% of the TCP tuples, steered to CPU 3: those frames' lookups use "
+         "outbound group ETH_MAX_TOTAL_FG + 3 (snapshot group nfg + 3 of n_out 5)", n_out=5, fdir_frac=0.4, cpu=3)
 
 
 if __name__ == "__main__":

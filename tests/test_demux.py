@@ -16,15 +16,27 @@ from oracle import oracle
 KEY = traces.RSS_KEY
 
 
+def _n_out(g):
+    return int(g["n_out"]) if "n_out" in g else 0
+
+
 def _oracle(g, rec=None):
     return oracle.demux_batch(int(g["nfg"]), g["active_start"], g["active"], g["tw_start"], g["tw"], g["listen"],
                               int(g["dev_idx"]) * 512, g["blob"], g["off"], g["len"], 0,
-                              g["rec"] if rec is None else rec)
+                              g["rec"] if rec is None else rec, n_out=_n_out(g))
 
 
 def _tables(g):
     return demux.DemuxTables(int(g["nfg"]), g["active_start"], g["active"].view(demux.PCB_DTYPE),
-                             g["tw_start"], g["tw"].view(demux.PCB_DTYPE), g["listen"].view(demux.LISTEN_DTYPE))
+                             g["tw_start"], g["tw"].view(demux.PCB_DTYPE), g["listen"].view(demux.LISTEN_DTYPE),
+                             _n_out(g))
+
+
+def _set_fdir(eng, g):
+    """The golden's flow-director filters (the fdir fixture), on the engine
+    that recomputes its RX records."""
+    if "fdir" in g:
+        eng.set_fdir(np.ascontiguousarray(g["fdir"]).view(ixgrx.FDIR_DTYPE).reshape(-1), int(g["fdir_cpu"]))
 
 
 def _diff(got, exp, what):
@@ -44,6 +56,11 @@ def test_golden_covers_every_outcome():
     for name in ("demux_default", "demux_nolisten_nfg64"):
         kinds |= set(np.unique(load_golden(name)["demux"][:, 4]).tolist())
     assert kinds == {demux.D_NONE, demux.D_ACTIVE, demux.D_TIMEWAIT, demux.D_LISTEN, demux.D_RESET, demux.D_DROP}
+    # flow-director frames (outbound groups) reach ACTIVE and TIME-WAIT PCBs
+    g = load_golden("demux_fdir_outbound")
+    fg = g["rec"][:, 0].astype(np.int64) | (g["rec"][:, 1].astype(np.int64) << 8)
+    out = set(np.unique(g["demux"][fg >= ixgrx.IXG_ETH_MAX_TOTAL_FG, 4]).tolist())
+    assert {demux.D_ACTIVE, demux.D_TIMEWAIT} <= out
 
 
 def test_listen_last_entry_quirk():
@@ -92,7 +109,8 @@ def test_flow_placement_matches_reference_records(golden_demux):
     fg, bucket = demux.flow_of(cfg, rip, lip, rp, lp)
     fg_ref = (rec[tcp, 0].astype(np.int64) | (rec[tcp, 1].astype(np.int64) << 8)) - 512 * int(g["dev_idx"])
     bk_ref = rec[tcp, 12].astype(np.int64) | (rec[tcp, 13].astype(np.int64) << 8)
-    assert (fg == fg_ref).all() and (bucket == bk_ref).all()
+    rss = (rec[tcp, 3] & ixgrx.RF_FDIR) == 0
+    assert (fg[rss] == fg_ref[rss]).all() and (bucket == bk_ref).all()
 
 
 # ---- GPU ------------------------------------------------------------------
@@ -220,6 +238,7 @@ def test_gpu_fused_golden(golden_demux, mode):
     eng = _engine_in_mode(ixgrx.Config(bytes(g["key"]), int(g["nb_rx_fgs"]), int(g["dev_idx"]), 0), mode)
     try:
         demux.load(eng, _tables(g))
+        _set_fdir(eng, g)
         rec, out = _fused_dev(eng, g["blob"], g["off"], g["len"], 0, len(g["len"]))
         assert (rec == g["rec"]).all()
         _diff(out, g["demux"], g["name"] + " fused " + mode)
@@ -245,5 +264,53 @@ def test_gpu_fused_vs_oracle(kind, n, listen, mode):
         exp = oracle.demux_batch(tabs.nfg, tabs.active_start, tabs.active, tabs.tw_start, tabs.tw, tabs.listen,
                                  512, tr.blob, tr.off, tr.len, tr.stride, er)
         _diff(out, exp, f"{kind} fused {mode}")
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["auto", "general"])
+@pytest.mark.parametrize("kind", ["tcp64", "imix"])
+def test_gpu_fdir_outbound_groups(kind, mode):
+    """Frames the flow director steers (ixg_rx_set_fdir) carry the CPU's
+    outbound group ETH_MAX_TOTAL_FG + cpu; their PCB lookup must use that
+    group's active and TIME-WAIT lists (tcp_in.c:249,260 on cur_fg =
+    fgs[pkt->fg_id]), which the snapshot holds after the local groups. Fused
+    and separate demux against the oracle, with matching outbound PCBs."""
+    import torch
+    rng = np.random.default_rng(0xFD1)
+    tr = traces.make_trace(kind, 100000, seed=0x1BD200)
+    cfg = ixgrx.Config(KEY, 128, 1, 0)
+    offs = tr.offsets().astype(np.int64)
+    b = tr.blob
+    tcp = np.nonzero(b[offs + 23] == 6)[0]
+    keys = demux.tcp_keys(b, offs[tcp])
+    keys["id"] = np.arange(tcp.size) + 1
+    pick = rng.random(tcp.size) < 0.25
+    filt = np.zeros(int(pick.sum()), ixgrx.FDIR_DTYPE)
+    filt["src_ip"], filt["dst_ip"] = keys["remote_ip"][pick], keys["local_ip"][pick]
+    filt["src_port"], filt["dst_port"] = keys["remote_port"][pick], keys["local_port"][pick]
+    cpu, n_out = 2, 4
+    out_keys = keys[pick]
+    u = rng.random(out_keys.size)
+    oa, ot = out_keys[u < 0.7], out_keys[(u >= 0.7) & (u < 0.85)]
+    local = keys[~pick][:5000]
+    lis = np.array([(0, int(keys["local_port"][0]), 0, 77, 0)], dtype=demux.LISTEN_DTYPE)
+    tabs = demux.DemuxTables.build(cfg, local, np.zeros(0, demux.PCB_DTYPE), lis,
+                                   outbound=(oa, ot, np.full(oa.size, cpu), np.full(ot.size, cpu)), n_out=n_out)
+    er, _ = oracle.rx_batch(KEY, 128, 1, 0, tr.blob, tr.off, tr.len, tr.stride, threads=8, fdir=filt, cpu_id=cpu)
+    exp = oracle.demux_batch(tabs.nfg, tabs.active_start, tabs.active, tabs.tw_start, tabs.tw, tabs.listen, 512,
+                             tr.blob, tr.off, tr.len, tr.stride, er, n_out=n_out)
+    kinds = exp[(er[:, 0].astype(np.int64) | (er[:, 1].astype(np.int64) << 8)) >= 8192, 4]
+    assert (kinds == demux.D_ACTIVE).sum() > 1000 and (kinds == demux.D_TIMEWAIT).sum() > 100
+    eng = _engine_in_mode(cfg, mode)
+    try:
+        demux.load(eng, tabs)
+        eng.set_fdir(filt, cpu)
+        rec, out = _fused_dev(eng, tr.blob, tr.off, tr.len, tr.stride, tr.n)
+        assert (rec == er).all()
+        _diff(out, exp, f"{kind} fdir fused {mode}")
+        out2 = demux.batch_host(eng, tr.blob, tr.off, tr.len, tr.stride, er)
+        _diff(out2, exp, f"{kind} fdir separate {mode}")
     finally:
         eng.close()

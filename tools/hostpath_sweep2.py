@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Asynchronous host path, staged (DIRECT) vs zero copy (registered mbufs),
+1/4/8/16 threads, 2 s per point (GPU box)."""
+import json
+import os
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+
+
+def main():
+    import bench
+    from ix_amd import traces
+    kind = sys.argv[1] if len(sys.argv) > 1 else "tcp64"
+    pool = traces.make_trace(kind, 1 << 16, seed=0x1BF000)
+    f = os.path.join(tempfile.mkdtemp(), "frames.bin")
+    bench.write_frames_file(pool, f)
+    for reg in (0, 1):
+        for t in (1, 4, 8, 16):
+            for bf in (4096, 16384):
+                r = bench._loop_run(f, "loop", 120, threads=t, seconds=2.0, batch=64, arena=1 << 16,
+                                    cfg_frames=bf, cfg_bytes=bf * 128, register=reg)
+                print(json.dumps({"kind": kind, "zero_copy": reg, "threads": t, "batch_frames": bf,
+                                  "mpps": r.get("mpps"), "lat_p50": r.get("latency_us", {}).get("p50"),
+                                  "lat_p99": r.get("latency_us", {}).get("p99"), "err": r.get("error")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
