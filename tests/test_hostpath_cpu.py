@@ -216,12 +216,15 @@ def test_async_zero_copy(fake, kind):
             eng.register_memory(arena.ctypes.data + 4096, 1 << 16)  # overlaps
         n0 = fake.lib.fakehip_inplace_frames()
         m, r = _loop(eng, ptrs, rng)
-        assert fake.lib.fakehip_inplace_frames() - n0 == len(ptrs)  # every frame read in place
+        # every frame whose mbuf (and the tail bytes) lies inside the region is read in place
+        hi = arena.ctypes.data + arena.nbytes
+        inside = (ptrs.astype(np.int64) + 2112 + 64 <= hi)
+        assert fake.lib.fakehip_inplace_frames() - n0 == int(inside.sum()) >= len(ptrs) - 1
         assert np.array_equal(m, ptrs)
         assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
         n1 = fake.lib.fakehip_inplace_frames()
         m, r = _loop(eng, mix, rng)
-        assert fake.lib.fakehip_inplace_frames() - n1 == int((mix == ptrs).sum())
+        assert fake.lib.fakehip_inplace_frames() - n1 == int(((mix == ptrs) & (mix.astype(np.int64) + 2176 <= hi)).sum())
         assert np.array_equal(m, mix)
         assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(mix))
         eng.unregister_memory(arena.ctypes.data)
