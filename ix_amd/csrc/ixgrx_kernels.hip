@@ -747,8 +747,8 @@ DEV uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // lookups, and a verdict that can only be TCP or a checksum drop
 // (ixgbe.c:312-324 then tcp_in.c:189-241). The caller guarantees per lane:
 // proto 6, no fragment bits, 14 + ipl <= L, doff*4 <= ipl - 20 (TCPOK).
-DEV void lean_tcp(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, int lane,
-                  const uint32_t (&d)[kPrefixDw], uint32_t ipl, __amdgpu_buffer_rsrc_t out) {
+DEV Rec lean_tcp(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, int lane,
+                 const uint32_t (&d)[kPrefixDw], uint32_t ipl, __amdgpu_buffer_rsrc_t out) {
   // ---- IP header checksum: hi16(d3) + d4..d7 + lo16(d8) (chksum_internet) ----
   Adc ip(d[3] >> 16, d[4]);
   ip.add(d[5]);
@@ -819,6 +819,15 @@ DEV void lean_tcp(const KParams& p, const uint64_t* __restrict__ T, uint32_t i, 
   // (out covers the chunk's valid frames only: the stores of other lanes drop)
   __builtin_amdgcn_raw_buffer_store_b128(u32x4{r.w0, r.w1, r.w2, r.w3}, out, 16 * lane, 0, kAuxNT);
   if (p.csum && i < p.n) p.csum[i] = ((~ipf) & 0xffffu) | (((~l4f) & 0xffffu) << 16);
+  return r;
+}
+
+// the 4-tuple of a lean chunk's frame (bytes 26..37) as the fused demux takes
+// it: raw IPs, ports host order (sport | dport << 16)
+DEV void lean_tuple(const uint32_t (&d)[kPrefixDw], uint32_t& src, uint32_t& dst, uint32_t& ports) {
+  src = (d[6] >> 16) | (d[7] << 16);
+  dst = (d[7] >> 16) | (d[8] << 16);
+  ports = bswap16(d[8] >> 16) | (bswap16(d[9] & 0xffffu) << 16);
 }
 
 // LDS (address space 3) pointers: through generic pointers these would be
@@ -1682,27 +1691,34 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     }
     if (DRAIN && kth < 64u && !all_fast) dmask |= 1ull << kth;
     kth++;
+    // the lean path (lean_tcp) when every frame is a TCP segment tcp_input
+    // accepts and all share one IP total length
+    const uint32_t ipl = __builtin_amdgcn_readfirstlane(ip_len);
+    const bool tcpok = (d[5] & 0xff00ff3fu) == 0x06000000u && 14u + ipl <= Lc && ((d[11] >> 18) & 0x3cu) <= ipl - 20u;
+    const bool lean = all_fast && ipl >= 40u && wave_all(!valid || (ip_len == ipl && tcpok));
+    const uint32_t rem = p.n - c * 64u < 64u ? p.n - c * 64u : 64u;
     if (DMX) {
       // (a deferred chunk's records and demux records are the general kernel's)
-      LaneState s;
       Rec r{0u, 0u, 0u, 0u};
-      if (all_fast) {
+      uint32_t src = 0, dst = 0, ports = 0;
+      if (lean) {
+        r = lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * rem));
+        lean_tuple(d, src, dst, ports);
+      } else if (all_fast) {
+        LaneState s;
         lane_parse<kShapeFixed, kFastDw>(p, Tab64{T}, d, Lc, s);
         const uint32_t r4 = l4_residual(s);
         r = make_record<true>(p, d, Lc, s, r4);
         if (valid) store_record<true>(p, i, r, s.ip_res, r4);
+        src = s.src;
+        dst = s.dst;
+        ports = s.ports;
       }
-      dmx_issue(p, all_fast && valid, i, r, s.src, s.dst, s.ports, lane, pend);
+      dmx_issue(p, all_fast && valid, i, r, src, dst, ports, lane, pend);
+    } else if (lean) {
+      lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * rem));
     } else if (all_fast) {
-      // the lean path (lean_tcp) when every frame is a TCP segment
-      // tcp_input accepts and all share one IP total length
-      const uint32_t ipl = __builtin_amdgcn_readfirstlane(ip_len);
-      const bool tcpok = (d[5] & 0xff00ff3fu) == 0x06000000u && 14u + ipl <= Lc &&
-                         ((d[11] >> 18) & 0x3cu) <= ipl - 20u;
-      if (ipl >= 40u && wave_all(!valid || (ip_len == ipl && tcpok)))
-        lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * (p.n - c * 64u < 64u ? p.n - c * 64u : 64u)));
-      else
-        process_fast(p, T, i, valid, Lc, d);
+      process_fast(p, T, i, valid, Lc, d);
     }
     // the next iteration's LDS writes must not pass this one's reads
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1837,7 +1853,9 @@ DEV void general_body(const KParams& p) {
   // (in general: the wave's j-th chunk is ((j / G) nw + w) G + j % G, runs
   // of G consecutive chunks dealt out round-robin; G = 64 or 1)
   const uint32_t wv0 = blockIdx.x * kWaves + wave;
-  const uint64_t G = CLS == IXG_CLS_LONG && launch_big(p) ? kRunBig : kRun;
+  // (frames in host memory: one chunk per wave, latency-bound; the grid has
+  // one wave per chunk, ixgrx_launch)
+  const uint64_t G = p.host_mem || (CLS == IXG_CLS_LONG && launch_big(p)) ? kRunBig : kRun;
   for (uint32_t it = 0; ((uint64_t)64u * kQGroups * it / G * nw + wv0) * G < nchunks; it++) {
     uint32_t nq = 0;
 #pragma unroll
@@ -3180,7 +3198,8 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   }
 #endif
   const kern_fn kg = k_gen[gv][lay];
-  hipLaunchKernelGGL(kg, dim3(grid_for(kg, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
+  hipLaunchKernelGGL(kg, dim3(grid_for(kg, p.host_mem ? wave_blocks : group_blocks, ncu, sh6)), dim3(kBlock), sh6,
+                     (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
 
