@@ -19,9 +19,6 @@ struct ixg_dstate {
 	size_t defer_cap;
 	uint32_t *d_present; /* [IXG_PRESENT_WORDS] (ixg_kparams.present) */
 	uint32_t epoch;      /* last launch's stamp */
-	uint32_t *d_tail;    /* the parse / tail split: 32 B per frame (ixg_kparams.tail) */
-	uint64_t *d_tmeta;   /* 8 B per chunk (ixg_kparams.tmeta) */
-	size_t tail_cap;     /* frames d_tail holds */
 };
 
 #define IXG_MAX_REGIONS 32u
@@ -64,9 +61,6 @@ struct ixg_ctx {
 	uint32_t crc_const;
 	uint32_t ncu;        /* compute units: persistent grids are sized from it */
 	int force_general;   /* IXG_SPLIT_GENERAL: skip the fixed-shape kernel (ixg_rx_set_split) */
-	int variant;         /* kernel variant selector: 0 in the product library; A/B
-	                        builds (-DIXGRX_AB, tools/build_variant.sh) read it
-	                        from IXGRX_*_VARIANT */
 	uint32_t force_mode; /* IXG_MODE_* forced by ixg_rx_set_split, or IXG_MODE_AUTO */
 	struct ixg_dstate ds; /* the synchronous and device-resident paths' */
 	struct ixg_slot slot[IXG_SLOTS];

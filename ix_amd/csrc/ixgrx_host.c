@@ -103,8 +103,6 @@ const char *ixg_strerror(int err)
 void ixg_dstate_free(struct ixg_dstate *ds)
 {
 	hipFree(ds->d_defer);
-	hipFree(ds->d_tail);
-	hipFree(ds->d_tmeta);
 	hipFree(ds->d_present);
 	memset(ds, 0, sizeof(*ds));
 }
@@ -182,19 +180,6 @@ int ixg_rx_init(const struct ixg_rx_cfg *cfg, int device, void **out)
 	if (hipGetDeviceProperties(&prop, device) != hipSuccess)
 		goto fail;
 	c->force_mode = IXG_MODE_AUTO;
-#ifdef IXGRX_AB
-	{
-		/* A/B builds only (never the product library) */
-		const char *e = getenv("IXGRX_FAST_VARIANT");
-		c->variant = e ? (atoi(e) & 0xff) : 0;
-		e = getenv("IXGRX_GEN_VARIANT");
-		c->variant |= e ? ((atoi(e) & 0xff) << 8) : 0;
-		e = getenv("IXGRX_SHORT_VARIANT");
-		c->variant |= e ? ((atoi(e) & 0xff) << 16) : 0;
-		e = getenv("IXGRX_FLAT");  /* bit 30: the flat long kernel */
-		c->variant |= (e && atoi(e)) ? (1 << 30) : 0;
-	}
-#endif
 	c->ncu = (uint32_t)prop.multiProcessorCount;
 	uint64_t *tab = (uint64_t *)malloc(12 * 256 * sizeof(uint64_t));
 	if (!tab) {
@@ -301,22 +286,6 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 			HIPCHK(hipMalloc((void **)&ds->d_defer, cap));
 			ds->defer_cap = cap;
 		}
-#ifdef IXGRX_AB
-		/* the parse / tail split's buffers (A/B builds only) */
-		if (n > ds->tail_cap) {
-			hipFree(ds->d_tail);
-			hipFree(ds->d_tmeta);
-			ds->d_tail = NULL;
-			ds->d_tmeta = NULL;
-			ds->tail_cap = 0;
-			size_t cap = ((size_t)n + n / 4 + 4096) & ~(size_t)63;
-			HIPCHK(hipMalloc((void **)&ds->d_tail, cap * 32));
-			HIPCHK(hipMalloc((void **)&ds->d_tmeta, cap / 64 * 8));
-			ds->tail_cap = cap;
-		}
-		p.tail = ds->d_tail;
-		p.tmeta = ds->d_tmeta;
-#endif
 		p.defer = ds->d_defer;
 		p.present = ds->d_present;
 		if (++ds->epoch == 0)
@@ -324,7 +293,7 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		p.epoch = ds->epoch;
 		p.force_mode = c->force_mode;
 	}
-	return ixgrx_launch(&p, c->variant, c->ncu, s) == 0 ? 0 : -EIO;
+	return ixgrx_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
 }
 
 /* the table: header {mask, fg, 0, 0} + slots (ixgrx_internal.h); the

@@ -37,22 +37,8 @@ struct ixg_kparams {
 	                          launch; present[0] == epoch iff the sampler (or
 	                          the self-sampling short kernel) ran,
 	                          and then present[3] is the launch's IXG_MODE_*;
-	                          present[4] == epoch iff the parse kernel left
-	                          tails for the tail kernel; present[5] == epoch
-	                          iff the flat kernel walked every chunk
-	                          (IXG_MODE_LONG) and flagged the ones it left;
 	                          present[6] != 0: most sampled chunks are big
 	                          (the long kernel walks its chunks strided) */
-	/* the parse / tail split of the long class (with defer): the parse
-	 * kernel leaves each long L4 segment's whole 16-byte pieces past the
-	 * prefix to the tail kernel. tail: 2 x u32x4 per frame index {frame
-	 * offset lo, hi, seg_end | ip_res << 16, partial sum}, {the record if
-	 * the L4 check fails}; tmeta: per chunk the mask of its lanes with a
-	 * tail, written for every chunk the parse kernel takes (the tail kernel
-	 * takes the same chunks: no stale mask is ever read, graph replays
-	 * included) */
-	uint32_t *tail;
-	uint64_t *tmeta;
 	uint32_t epoch;        /* per-launch stamp (never 0) */
 	uint32_t force_mode;   /* IXG_MODE_* for the sampler to write instead of
 	                          sampling (tests), or IXG_MODE_AUTO */
@@ -82,8 +68,6 @@ struct ixg_kparams {
 	uint32_t overlap;      /* fixed-stride batches: frames may run up to 64 bytes
 	                          past their slot (the host paths' staging, whose
 	                          skipped MAC bytes overlap the previous frame) */
-	uint32_t flat_cap;     /* the flat long kernel: 16-byte pieces of LDS per
-	                          wave (set by ixgrx_launch for that kernel) */
 	uint32_t self_sample;  /* set by ixgrx_launch for the span-staged short
 	                          kernel when it runs first: it samples the
 	                          launch's mode itself and publishes it */
@@ -148,7 +132,7 @@ IXG_HD static inline uint32_t ixg_demux_group(uint32_t fg_id, uint32_t fg_base, 
 /* enqueue one batch: the fixed-shape kernel (when p->defer) and the general
  * kernel; grids are sized from the device's CU count and each kernel's
  * occupancy */
-int ixgrx_launch(const void *params, int variant, uint32_t ncu, void *stream);
+int ixgrx_launch(const void *params, uint32_t ncu, void *stream);
 uint32_t ixgrx_kparams_size(void);
 uint32_t ixgrx_block(void);
 

@@ -1142,11 +1142,7 @@ constexpr int kModeLong = 0, kModeFirst = 2;
 // (Dn -> Pn) is loaded here, after this chunk's last streaming round is
 // issued (its registers free by then), instead of after this chunk, where
 // the next chunk waited out its whole latency
-// SPLIT (the parse kernel of the parse / tail split): no streaming rounds;
-// a long segment's pending sum, offsets and failure record go to p.tail for
-// the tail kernel, the record for a passing check is stored now, and the
-// chunk's tail mask to p.tmeta. Returns true when the chunk left tails.
-template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false, bool DMX = true, bool SPLIT = false>
+template <bool OFFS, int MODE, bool BIG, int SM = 0, bool LATE = false, bool DMX = true>
 DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane,
                        const WaveLds& w, const GDesc& g, const GPre& x, const GDesc* Dn = nullptr,
                        GPre* Pn = nullptr) {
@@ -1190,7 +1186,6 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   const bool lng = !SHORT && strm && (pend > (uint32_t)kStreamBase || !short_tail);
   if (strm && !lng) s.l4_acc += piece_sum(v96, (int)rr);
   const uint64_t m = SHORT ? 0ull : __ballot(lng);
-  if (SPLIT && !m && lane == 0) p.tmeta[chunk] = 0ull;
   if (SHORT || !m) {  // no long segment in this chunk (wave-uniform)
     if (LATE) gen_pre<false, BIG>(p, *Dn, lane, *Pn);
     if (valid) {
@@ -1208,21 +1203,6 @@ DEV bool general_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_
   Rec rbad = make_record(p, d, L, s, 1u);
   uint32_t acc32 = fold32(s.l4_acc), ip_res = s.ip_res;
   uint32_t tsrc = s.src, tdst = s.dst, tports = s.ports;
-  if (SPLIT) {
-    if (lane == 0) p.tmeta[chunk] = m;
-    if (valid) {
-      if (lng) {
-        u32x4* t = reinterpret_cast<u32x4*>(p.tail) + 2u * (size_t)i;
-        t[0] = u32x4{(uint32_t)off, (uint32_t)(off >> 32), s.seg_end | (ip_res << 16), acc32};
-        t[1] = u32x4{rbad.w0, rbad.w1, rbad.w2, rbad.w3};
-        *reinterpret_cast<u32x4*>(p.out + i) = u32x4{rok.w0, rok.w1, rok.w2, rok.w3};  // (csum: the tail kernel)
-      } else {
-        store_record(p, i, rok, ip_res, r4);
-      }
-      store_demux<DMX>(p, i, rok, tsrc, tdst, tports);
-    }
-    return true;
-  }
   const u32x4 ve = load16(lng && rr != 0u, p.base + off + pend, p.zero + 16 * lane);
   // materialise these now, so the parse state (d[], s) is dead during the
   // streaming rounds instead of being kept live for sunk computations
@@ -1505,16 +1485,6 @@ DEV void fast_loop(const KParams& p, const uint64_t* __restrict__ T) {
 // _s: fixed-stride layout, _o: u64 offsets
 IXG_FAST_KERNEL(ixg_rx_fast_s, false, 1, 5)
 IXG_FAST_KERNEL(ixg_rx_fast_o, true, 1, 5)
-#ifdef IXGRX_AB
-// A/B builds only (tools/build_variant.sh; IXGRX_FAST_VARIANT): never in the
-// product library
-IXG_FAST_KERNEL(ixg_rx_fast_a2w4_s, false, 2, 4)
-IXG_FAST_KERNEL(ixg_rx_fast_a2w4_o, true, 2, 4)
-IXG_FAST_KERNEL(ixg_rx_fast_a2w5_s, false, 2, 5)
-IXG_FAST_KERNEL(ixg_rx_fast_a2w5_o, true, 2, 5)
-IXG_FAST_KERNEL(ixg_rx_fast_a1w4_s, false, 1, 4)
-IXG_FAST_KERNEL(ixg_rx_fast_a1w4_o, true, 1, 4)
-#endif
 
 // ---- fixed-shape kernel, coalesced (fixed stride <= 64 B) ---------------
 // A wave's 64 frames are one contiguous 64*stride-byte run. The wave loads
@@ -1530,6 +1500,11 @@ IXG_FAST_KERNEL(ixg_rx_fast_a1w4_o, true, 1, 4)
 // lies below (n-1)*stride + min(L_last, 64) <= lim - 64. A chunk past the
 // end reads the zero page (IXG_ZERO_PAGE = 4096 covers the 4 KiB image).
 // cc, nchunks and lim are wave-uniform (SGPRs)
+// s_waitcnt immediates (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4],
+// lgkmcnt [11:8]; a field at its maximum does not wait)
+constexpr uint32_t kGldsWait = 0x0F70;  // vmcnt(0)
+constexpr uint32_t kLdsWait = 0xC07F;   // lgkmcnt(0)
+
 DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t lim, int lane, u32x4 (&v)[4],
                      uint32_t& L) {
   const bool live = cc < nchunks;
@@ -1559,41 +1534,77 @@ DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t l
 // the next iteration, after that chunk's frame loads are issued. (Matched at
 // once, the wait for the line -- vmcnt is in order -- also waited for the
 // next chunk's frames, loaded just before: the prefetch became synchronous.)
+// The 64 lines of a chunk are loaded by 4 lanes each (16 lines of 64 B per
+// wave instruction, 4 instructions): a lane loading its own line made every
+// instruction touch 64 lines, 4 times over, and the L1's per-line work, not
+// the bytes, bounded the kernel. The pieces are exchanged through the wave's
+// LDS buffer when the lookups are matched.
 struct PendDmx {
-  u32x4 line[4];  // the bucket line (zero page when none)
-  uint32_t i;     // frame index; kNoDmx when the lane stores nothing
-  uint32_t fg, tflags, src, dst, ports;  // fg = kNoDmx: not an IXG_V_TCP record
+  u32x4 piece[4];  // piece k: bytes 16*(lane&3).. of the line of lane (lane>>2) + 16k
+  uint32_t c;      // the chunk (wave-uniform); kNoDmx: nothing pending
+  uint32_t fgt;    // group | TCP flags << 24; group kNotTcp / kNoFrame below
+  uint32_t src, dst, ports;
 };
 constexpr uint32_t kNoDmx = 0xffffffffu;
+constexpr uint32_t kNotTcp = 0xffffffu;   // a valid frame that is not IXG_V_TCP
+constexpr uint32_t kNoFrame = 0xfffffeu;  // past the batch, or a deferred chunk
 
 DEV ixgwalk::Tables dmx_tables(const KParams& p) {
   return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
 }
 
-// record r of frame i (valid lanes) -> pending lookup, line loads issued
-DEV void dmx_issue(const KParams& p, bool valid, uint32_t i, const Rec& r, uint32_t src, uint32_t dst, uint32_t ports,
+// record r of frame i of chunk c (valid lanes) -> pending lookup, the
+// chunk's bucket lines loaded
+DEV void dmx_issue(const KParams& p, bool valid, uint32_t c, const Rec& r, uint32_t src, uint32_t dst, uint32_t ports,
                    int lane, PendDmx& q) {
   const bool tcp = valid && ((r.w0 >> 16) & 0xffu) == IXG_V_TCP;
-  q.i = valid ? i : kNoDmx;
-  q.fg = tcp ? ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out) : kNoDmx;
-  q.tflags = (r.w3 >> 16) & 0xffu;
+  const uint32_t ng = p.nfg + p.n_out;
+  const uint32_t fg = tcp ? ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out) : kNoDmx;
+  const bool look = tcp && fg < ng;
+  q.c = c;
+  q.fgt = (valid ? (tcp ? (look ? fg : kNotTcp - 2u) : kNotTcp) : kNoFrame) | (((r.w3 >> 16) & 0xffu) << 24);
   q.src = src;
   q.dst = dst;
   q.ports = ports;
-  const u32x4* line = tcp ? ixgwalk::bucket_line(dmx_tables(p), q.fg, r.w3 & 0xffffu) : nullptr;
-  const u32x4* src4 = line ? line : reinterpret_cast<const u32x4*>(p.zero + 64 * lane);
+  // the line's index in the snapshot (past the end: no line, the loads of
+  // its pieces read 0 without touching memory)
+  const uint32_t line = look ? fg * IXG_PCB_BUCKETS + (r.w3 & 0xffffu) : ng * IXG_PCB_BUCKETS;
+  const __amdgpu_buffer_rsrc_t rs = rsrc(p.bline, ng * IXG_PCB_BUCKETS * 64u);
 #pragma unroll
-  for (int k = 0; k < 4; k++) q.line[k] = src4[k];
+  for (int k = 0; k < 4; k++) {
+    const uint32_t li = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * ((lane >> 2) + 16 * k), (int)line);
+    q.piece[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, li * 64u + 16u * (uint32_t)(lane & 3), 0, 0);
+  }
 }
 
-DEV void dmx_finish(const KParams& p, const PendDmx& q) {
-  if (q.i == kNoDmx) return;
+// match the pending lookups (buf: the wave's 4 KiB of LDS, free)
+DEV void dmx_finish(const KParams& p, const PendDmx& q, int lane, lds_u32* buf) {
+  if (q.c == kNoDmx) return;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    lds_u32* w = buf + 4 * (lane + 64 * k);  // = line (lane>>2)+16k, piece lane&3
+    w[0] = q.piece[k].x; w[1] = q.piece[k].y; w[2] = q.piece[k].z; w[3] = q.piece[k].w;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  u32x4 ln[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const lds_u32* r = buf + 16 * lane + 4 * k;
+    ln[k] = u32x4{r[0], r[1], r[2], r[3]};
+  }
+  // (the caller's next LDS writes must not pass these reads)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t g = q.fgt & 0xffffffu;
+  if (g == kNoFrame) return;
   uint32_t id = 0, kind = IXG_D_NONE;
-  if (q.fg != kNoDmx)
-    ixgwalk::walk_finish(dmx_tables(p), q.fg, q.tflags, q.src, q.dst, q.ports, q.line[0], q.line[1], q.line[2],
-                         q.line[3], id, kind);
+  if (g != kNotTcp)
+    ixgwalk::walk_finish(dmx_tables(p), g, q.fgt >> 24, q.src, q.dst, q.ports, ln[0], ln[1], ln[2], ln[3], id, kind);
   typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-  reinterpret_cast<u32x2v*>(p.dmx)[q.i] = u32x2v{id, kind};
+  reinterpret_cast<u32x2v*>(p.dmx)[q.c * 64u + (uint32_t)lane] = u32x2v{id, kind};
 }
 
 // A chunk the coalesced kernel could not take as fixed-shape, finished by
@@ -1646,18 +1657,18 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   u32x4 cur[4];
   uint32_t Lc, seen = 0;
   PendDmx pend;
-  if (DMX) pend.i = kNoDmx;
+  if (DMX) pend.c = kNoDmx;
   fastc_issue(p, c, nchunks, lim, lane, cur, Lc);
   for (;;) {
     const uint32_t cn = chunk_of(kth + 1);
     u32x4 nxt[4];
     uint32_t Ln;
     fastc_issue(p, cn, nchunks, lim, lane, nxt, Ln);
-    if (DMX) dmx_finish(p, pend);
+    if (DMX) dmx_finish(p, pend, lane, buf);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-      lds_u32* q = buf + 4 * (lane + 64 * k);
-      q[0] = cur[k].x; q[1] = cur[k].y; q[2] = cur[k].z; q[3] = cur[k].w;
+      lds_u32* w = buf + 4 * (lane + 64 * k);
+      w[0] = cur[k].x; w[1] = cur[k].y; w[2] = cur[k].z; w[3] = cur[k].w;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1714,7 +1725,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
         dst = s.dst;
         ports = s.ports;
       }
-      dmx_issue(p, all_fast && valid, i, r, src, dst, ports, lane, pend);
+      dmx_issue(p, all_fast && valid, c, r, src, dst, ports, lane, pend);
     } else if (lean) {
       lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * rem));
     } else if (all_fast) {
@@ -1730,7 +1741,7 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     for (int k = 0; k < 4; k++) cur[k] = nxt[k];
     Lc = Ln;
   }
-  if (DMX) dmx_finish(p, pend);
+  if (DMX) dmx_finish(p, pend, lane, buf);
   publish_classes(p, seen, lane);
   if (DRAIN) {
     // the wave's own deferred chunks (its first 64: a wave has ~8; the rest,
@@ -1762,12 +1773,11 @@ ixg_rx_fastc_dmx_s(KParams p) {
 // p.defer is null) one at a time.
 // Walk a wave's chunk list with descriptors two chunks ahead; EARLY: the
 // frame bytes one chunk ahead too, else loaded right before each chunk.
-template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false, bool BIG_OK = true, bool DMX = true,
-          bool SPLIT = false>
+template <bool OFFS, bool EARLY, int MODE, int SM = 0, bool LATE_OK = false, bool BIG_OK = true, bool DMX = true>
 DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const lds_u32* q,
                   uint32_t nq, int lane, GDesc D0) {
   constexpr bool GATE = MODE == kModeFirst;
-  constexpr bool BIG = BIG_OK && MODE == kModeLong && (!EARLY || SPLIT);
+  constexpr bool BIG = BIG_OK && MODE == kModeLong && !EARLY;
   bool deferred = false;
   uint32_t c0 = q[0], c1 = nq > 1 ? q[1] : kNoChunk;
   GDesc D1;
@@ -1781,7 +1791,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     GPre P1;
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     constexpr bool LATE = LATE_OK && !EARLY && MODE == kModeLong;
-    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE, DMX, SPLIT>(p, T, c0, lane, w, D0, P0, &D1, &P1);
+    deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE, DMX>(p, T, c0, lane, w, D0, P0, &D1, &P1);
     if (!EARLY && !LATE) gen_pre<GATE, BIG>(p, D1, lane, P1);
     c0 = c1;
     c1 = c2;
@@ -1798,7 +1808,7 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
 template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0, bool LATE = false, bool BIGOK = true,
-          int kWaves = 4, int kQGroups = 4, bool DMX = true, bool SPLIT = false>
+          int kWaves = 4, int kQGroups = 4, bool DMX = true>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
@@ -1814,10 +1824,7 @@ DEV void general_body(const KParams& p) {
   // a block with no deferred chunk exits before staging the tables (the
   // common case behind the fixed-shape kernel: 64 B frames)
   const uint32_t mode = launch_mode(p);
-  // (IXG_MODE_LONG behind the flat kernel: only the chunks it flagged)
-  const bool all = CLS == IXG_CLS_SHORT
-                       ? mode == IXG_MODE_SHORT
-                       : (p.defer == nullptr || (mode == IXG_MODE_LONG && p.present[5] != p.epoch));
+  const bool all = CLS == IXG_CLS_SHORT ? mode == IXG_MODE_SHORT : (p.defer == nullptr || mode == IXG_MODE_LONG);
   // (p.present is only read when the flags are in use: it is null with
   // p.defer when the general kernel runs alone)
   if (!all) {
@@ -1878,8 +1885,6 @@ DEV void general_body(const KParams& p) {
     gen_desc<OFFS>(p, q[0], lane, D0);
     if (CLS == IXG_CLS_SHORT)
       seen |= gen_walk<OFFS, SEARLY, kModeFirst, 0, false, true, DMX>(p, T, w, q, nq, lane, D0);
-    else if (SPLIT)
-      seen |= gen_walk<OFFS, SEARLY, kModeLong, SM, false, BIGOK, DMX, true>(p, T, w, q, nq, lane, D0);
     else if (!SEARLY || wave_any(D0.L > (uint32_t)kStreamBase + 32u))
       gen_walk<OFFS, false, kModeLong, SM, LATE, BIGOK, DMX>(p, T, w, q, nq, lane, D0);
     else
@@ -1887,109 +1892,7 @@ DEV void general_body(const KParams& p) {
     __builtin_amdgcn_wave_barrier();
   }
   if (CLS == IXG_CLS_SHORT) publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
-  if (SPLIT && seen && lane == 0) p.present[4] = p.epoch;
 }
-
-#ifdef IXGRX_AB
-// ---- the tail kernel (the parse / tail split of the long class) -----------
-// A/B builds only: measured slower than the one-kernel general path (C3
-// 1.82 vs 1.49 ms per launch: parse 0.75 ms + tail 1.08 ms; C4 2.64 vs
-// 2.38 ms), see DESIGN.md section 8.
-// The parse kernel (general_body<SPLIT>) leaves each long L4 segment's whole
-// 16-byte pieces past the prefix in p.tail; this kernel streams them with
-// no parse state live (the streaming rounds of general_chunk: medium
-// segments by 4-lane groups, the rest by 16-lane groups, two rounds in
-// flight), so it runs at a higher occupancy than the one-kernel general
-// path, whose parse registers capped it at 2 waves per SIMD. Per chunk with
-// tails: the owners' items into the wave's LDS list, the rounds, then each
-// owner folds its sum; a failing check stores the failure record the parse
-// kernel built over the passing one (and its demux record).
-template <bool DMX>
-DEV void tail_chunk(const KParams& p, const WaveLds& w, uint32_t chunk, int lane) {
-  const uint64_t meta = p.tmeta[chunk];  // one address: a broadcast
-  const uint64_t m = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(meta >> 32)) << 32) |
-                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)meta);
-  const bool lng = (m >> lane) & 1u;
-  const uint32_t i = chunk * 64u + (uint32_t)lane;
-  const u32x4* t = reinterpret_cast<const u32x4*>(p.tail) + 2u * (size_t)i;
-  const u32x4 q0 = *(lng ? t : reinterpret_cast<const u32x4*>(p.zero));
-  const uint64_t off = ((uint64_t)q0.y << 32) | q0.x;
-  const uint32_t seg_end = q0.z & 0xffffu, ip_res = q0.z >> 16, acc = q0.w;
-  const uint32_t tl = seg_end - (uint32_t)kStreamBase, rr = tl & 15u, pend = (uint32_t)kStreamBase + (tl & ~15u);
-  const bool lmed = lng && pend <= (uint32_t)kStreamBase + kMedSpan;
-  const uint64_t mm = __ballot(lmed), mb = m & ~mm;
-  const uint32_t nmed = (uint32_t)__popcll(mm), nlong = (uint32_t)__popcll(m);
-  if (lng) {
-    const uint64_t mine = lmed ? mm : mb;
-    const uint32_t at = (lmed ? 0u : nmed) +
-                        __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
-    w.list[at] = (uint32_t)lane;
-    w.end[lane] = pend;
-    w.offlo[lane] = (uint32_t)off;
-    w.offhi[lane] = (uint32_t)(off >> 32);
-  }
-  __builtin_amdgcn_wave_barrier();
-  const RoundPlan plan{nmed, nlong, (nmed + 64u / kMedG - 1u) / (64u / kMedG)};
-  const uint32_t R = plan.rm + (nlong - nmed + kRoundPk - 1) / kRoundPk;
-  const u32x4 ve = load16(lng && rr != 0u, p.base + off + pend, p.zero + 16 * lane);
-  Round A, B;
-  round_issue<1>(p, w, 0, plan, lane, A);
-#pragma clang loop unroll(disable)
-  for (uint32_t r = 0; r < R; r += 2) {
-    round_issue<1>(p, w, r + 1, plan, lane, B);
-    round_finish<1>(p, w, lane, A);
-    round_issue<1>(p, w, r + 2, plan, lane, A);
-    round_finish<1>(p, w, lane, B);
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (lng) {
-    const uint32_t res =
-        (~fold16(add1c(add1c(acc, w.sum[lane]), fold32(piece_sum(ve, (int)rr))))) & 0xffffu;
-    if (res != 0u) {
-      const u32x4 b = t[1];
-      *reinterpret_cast<u32x4*>(p.out + i) = b;
-      const Rec rb{b.x, b.y, b.z, b.w};
-      // (a failure record that is still IXG_V_TCP, IXG_F_NO_CSUM_DROP, has
-      // the passing record's lookup, stored by the parse kernel)
-      if (((b.x >> 16) & 0xffu) != IXG_V_TCP) store_demux<DMX>(p, i, rb, 0u, 0u, 0u);
-    }
-    if (p.csum) p.csum[i] = ip_res | (res << 16);
-  }
-  __builtin_amdgcn_wave_barrier();
-}
-
-template <int kTW, bool DMX>
-DEV void tail_body(const KParams& p) {
-  if (p.present[4] != p.epoch) return;  // the parse kernel left no tails
-  __shared__ uint32_t sh_list[kTW][64], sh_end[kTW][64], sh_offlo[kTW][64], sh_offhi[kTW][64], sh_sum[kTW][64],
-      sh_q[kTW][64];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nw = gridDim.x * kTW;
-  const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t ngroups = (nchunks + 63u) >> 6;
-  const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
-                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), nullptr, nullptr};
-  lds_u32* q = LDS(lds_u32, sh_q[wave]);
-  // the chunks the parse kernel took (general_body's selection), of which
-  // those with tails
-  const bool all = launch_mode(p) == IXG_MODE_LONG;
-  for (uint32_t g = blockIdx.x * kTW + wave; g < ngroups; g += nw) {
-    const uint32_t ci = g * 64u + (uint32_t)lane;
-    const bool sel = ci < nchunks && (all || p.defer[ci] == IXG_CLS_LONG);
-    const bool want = sel && p.tmeta[sel ? ci : 0u] != 0ull;
-    const uint64_t m = __ballot(want);
-    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t nq = (uint32_t)__popcll(m);
-    for (uint32_t j = 0; j < nq; j++) tail_chunk<DMX>(p, w, q[j], lane);
-  }
-}
-
-#define IXG_TAIL_KERNEL(NAME, WAVES, DMX)                                                           \
-  extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
-  NAME(KParams p) { tail_body<kWaves, DMX>(p); }
-IXG_TAIL_KERNEL(ixg_rx_tail, 4, true)
-#endif
 
 #define IXG_GEN_KERNEL(NAME, OFFS, CLS, WAVES, ...)                                                 \
   extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WAVES))) \
@@ -2004,14 +1907,6 @@ IXG_TAIL_KERNEL(ixg_rx_tail, 4, true)
 // A/B, and C3's FETCH_SIZE 6.64 -> 6.53 GB)
 IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
 IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
-#ifdef IXGRX_AB
-// the parse kernel of the parse / tail split (ixg_rx_tail streams the tails)
-IXG_GEN_KERNEL(ixg_rx_parse_s, false, IXG_CLS_LONG, 3, true, 1, false, false, 4, 4, true, true)
-IXG_GEN_KERNEL(ixg_rx_parse_o, true, IXG_CLS_LONG, 3, true, 1, false, false, 4, 4, true, true)
-// 4 waves/SIMD without the one-ahead prefix prefetch
-IXG_GEN_KERNEL(ixg_rx_parse4_s, false, IXG_CLS_LONG, 4, false, 1, false, false, 4, 4, true, true)
-IXG_GEN_KERNEL(ixg_rx_parse4_o, true, IXG_CLS_LONG, 4, false, 1, false, false, 4, 4, true, true)
-#endif
 // the short-class general kernel (no streaming rounds): 4 waves/SIMD
 // without the one-ahead prefix prefetch (128 VGPRs; C5 -3% against the
 // 3-wave prefetching build)
@@ -2037,8 +1932,6 @@ IXG_GENW_KERNEL(ixg_rx_short_w8d_o, 8, true, IXG_CLS_SHORT, 4, false, 0, false, 
 // Chunks that are not span-contiguous take per-lane loads.
 constexpr uint32_t kSpanMax = 6144;             // bytes per wave's span buffer
 constexpr int kSpanWaves = 16;                  // 1024-thread blocks, 1 per CU
-constexpr uint32_t kGldsWait = 0x0F70;          // s_waitcnt vmcnt(0) (gfx9 encoding)
-constexpr uint32_t kLdsWait = 0xC07F;           // s_waitcnt lgkmcnt(0)
 
 // 64-bit wave broadcasts (the builtins return int: each half is taken as
 // uint32_t, or a low word >= 2^31 would sign-extend over the high one)
@@ -2253,745 +2146,6 @@ DEV void short_span_body(const KParams& p) {
 IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
 IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
 
-// ---- the flat long kernel (A/B builds only) ---------------------------------
-// Measured slower than the general kernel on C3 (1.55-1.58 vs 1.48 ms per
-// launch in same-process A/Bs), kept for reference:
-// IXGRX_FLAT=1 in an A/B build runs it ahead of the general kernel.
-// Long chunks (a frame of IXG_SHORT_MAX bytes or more) whose frames lie in
-// one span of at most p.flat_cap 16-byte pieces (packed batches: C3's IMIX)
-// sum their L4 tails without any per-segment streaming. The wave sweeps the
-// chunk's whole span [sb, se) in rows of 64 consecutive pieces (1 KiB per
-// wave instruction, fully coalesced, every byte fetched once) and stores
-// each piece's one's complement sum in LDS; a lane-blocked scan turns those
-// into exclusive prefix sums P(k) of the span's 32-bit words. One's
-// complement sums are sums mod 2^32 - 1, so a segment's tail [96, seg_end)
-// is P(seg_end) - P(96) (add the complement), each P at a dword boundary
-// inside a piece completed from the lane's own prefix (byte 96) or the piece
-// holding the segment end (one 16-byte load). The parse is the span
-// kernel's (per-lane prefix loads of bytes 12..95, issued right after the
-// first sweep rows). Chunks that are not span-contiguous, or whose span
-// exceeds the LDS, are flagged for the general kernel.
-#ifdef IXGRX_AB
-constexpr int kFlatWaves = 16;  // 1024-thread blocks, one per CU
-constexpr int kFlatU = 2;       // rows per sweep batch (two batches in flight)
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-
-// one's complement (end-around carry) sum of a piece's four dwords
-DEV uint32_t piece1c(const u32x4& v) {
-  uint32_t a = v.x;
-  asm("v_add_co_u32 %0, vcc, %0, %1\n\t"
-      "v_addc_co_u32 %0, vcc, %0, %2, vcc\n\t"
-      "v_addc_co_u32 %0, vcc, %0, %3, vcc\n\t"
-      "v_addc_co_u32 %0, vcc, %0, 0, vcc"
-      : "+v"(a)
-      : "v"(v.y), "v"(v.z), "v"(v.w)
-      : "vcc");
-  return a;
-}
-
-// a sweep batch: rows [r0, r0 + kFlatU) of the span, raw buffer loads
-// through a descriptor bounded to the span (pieces past it read 0 without a
-// memory access); the row offset is a scalar, the lane's a constant
-DEV void flat_issue(__amdgpu_buffer_rsrc_t rs, uint32_t r0, int lane, u32x4 (&v)[kFlatU]) {
-#pragma unroll
-  for (int u = 0; u < kFlatU; u++)
-    v[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane, (int)(1024u * (r0 + (uint32_t)u)), 0);
-}
-
-// (rows past R, the span's last, are not stored: they sum to zero)
-DEV void flat_consume(lds_u32* S, uint32_t r0, uint32_t R, int lane, const u32x4 (&v)[kFlatU]) {
-#pragma unroll
-  for (int u = 0; u < kFlatU; u++)
-    if (r0 + (uint32_t)u < R) S[64u * (r0 + (uint32_t)u) + (uint32_t)lane] = piece1c(v[u]);
-}
-
-DEV void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// A chunk's head: its span and, when it fits, its first sweep batch and
-// its prefixes in flight. The walk issues the next chunk's head as soon as
-// the current chunk's sweep has been consumed, so those loads overlap the
-// current chunk's prefix sums and records.
-struct FlatHead {
-  uint32_t chunk;  // kNoChunk: none
-  bool ok;         // fits (else flagged for the general kernel)
-  uint64_t sb;     // span start (16-aligned, relative to p.base)
-  uint32_t npc;    // 16-byte pieces in the span
-  GDesc g;
-  u32x4 A[kFlatU];
-  uint32_t d[kPrefixDw];
-};
-
-template <bool OFFS>
-DEV void flat_head(const KParams& p, uint32_t chunk, const GDesc& g, int lane, FlatHead& h) {
-  h.chunk = chunk;
-  h.g = g;
-  h.ok = false;
-  if (chunk == kNoChunk) return;
-  const uint32_t L = g.L;  // 0 past the batch end
-  // the span: lane 0's frame starts it, the last valid lane's frame ends it,
-  // and every frame lies inside (ascending offsets: packed batches)
-  const uint32_t nv = p.n - chunk * 64u < 64u ? p.n - chunk * 64u : 64u;
-  const uint64_t b0 = rfl64(g.off);
-  const uint64_t end = g.off + L;
-  const uint64_t eL = rl64(end, nv - 1u);
-  const uint64_t sb = b0 & ~15ull;
-  if (!wave_all(L == 0u || (g.off >= b0 && end <= eL)) || eL - sb > 16ull * p.flat_cap) return;
-  const uint32_t npc = (uint32_t)((eL - sb + 15u) >> 4);
-  // R rows of 64 pieces; lane blocks of M pieces (M % 4 == 0, M <= 32)
-  // cover [0, npc] (P(npc) is the total): the blocks starting at or before
-  // npc end before 64 (R + 1), and row R is zeroed
-  if (64u * (((npc + 63u) >> 6) + 1u) > p.flat_cap) return;
-  h.ok = true;
-  h.sb = sb;
-  h.npc = npc;
-  // sweep batch 0, then the prefixes (their lines are among the rows')
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.base + sb), 0, (int)(16u * npc), 0x00020000);
-  flat_issue(rs, 0u, lane, h.A);
-  load_prefix<0, 6>(p.base + g.off, L, reinterpret_cast<const uint8_t*>(p.tab), h.d);
-}
-
-// One chunk whose head h fits; issues the head of chunk `next` (descriptors
-// gn) into h before its prefix sums.
-template <bool OFFS>
-DEV void flat_chunk(const KParams& p, const Tab64& tab, const lds_u32* t6, lds_u32* S, lds_u32* Bs, int lane,
-                    FlatHead& h, uint32_t next, const GDesc& gn) {
-  const uint32_t chunk = h.chunk;
-  const uint32_t i = chunk * 64u + (uint32_t)lane;
-  const bool valid = i < p.n;
-  const uint32_t L = h.g.L;
-  const uint64_t off = h.g.off, sb = h.sb;
-  const uint32_t npc = h.npc;
-  const uint32_t R = (npc + 63u) >> 6;
-  const uint32_t M = (((npc + 64u) >> 6) + 3u) & ~3u;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(p.base + sb), 0, (int)(16u * npc), 0x00020000);
-  flat_consume(S, 0u, R, lane, h.A);
-
-  // ---- parse ----
-  LaneState st;
-  parse_dispatch(p, tab, h.d, L, valid, st, t6);
-  const bool strm = valid && st.stream;  // segment ending past byte 96
-  const uint32_t r4 = strm ? 0u : l4_residual(st);
-  Rec rok = make_record(p, h.d, L, st, r4);
-  Rec rbad = make_record(p, h.d, L, st, 1u);
-  uint32_t acc32 = fold32(st.l4_acc), ip_res = st.ip_res;
-  const uint32_t kind = (uint32_t)st.l4_kind, seg_end = st.seg_end;
-  // span positions of byte 96 and of the segment end; the dwords of byte
-  // 96's piece before it are the prefix's last (96 - 16 k_x) / 4
-  const uint32_t rel = (uint32_t)(off - sb);
-  uint32_t x = rel + (uint32_t)kStreamBase, y = rel + seg_end;
-  const uint32_t rx = (x & 15u) >> 2;
-  uint32_t px = rx >= 3u ? h.d[21] : 0u;
-  px = add1c(px, rx >= 2u ? h.d[22] : 0u);
-  px = add1c(px, rx >= 1u ? h.d[23] : 0u);
-  const u32x4 ve = load16(strm && (y & 15u) != 0u, p.base + sb + (y & ~15u), p.zero + 16 * lane);
-  asm volatile("" : "+v"(rok.w0), "+v"(rok.w1), "+v"(rok.w2), "+v"(rok.w3));
-  asm volatile("" : "+v"(rbad.w0), "+v"(rbad.w1), "+v"(rbad.w2), "+v"(rbad.w3));
-  asm volatile("" : "+v"(acc32), "+v"(ip_res), "+v"(px), "+v"(x), "+v"(y));
-
-  // ---- the rest of the sweep: two batches in flight, each issued a full
-  // batch ahead of its use ----
-  u32x4 A[kFlatU], B[kFlatU];
-  flat_issue(rs, kFlatU, lane, B);
-  flat_issue(rs, 2u * kFlatU, lane, A);
-#pragma clang loop unroll(disable)
-  for (uint32_t r0 = kFlatU; r0 < R; r0 += 2u * kFlatU) {
-    flat_consume(S, r0, R, lane, B);
-    flat_issue(rs, r0 + 2u * kFlatU, lane, B);
-    flat_consume(S, r0 + kFlatU, R, lane, A);
-    flat_issue(rs, r0 + 3u * kFlatU, lane, A);
-  }
-  S[64u * R + (uint32_t)lane] = 0u;
-  // the next chunk's head: its loads overlap the rest of this chunk
-  flat_head<OFFS>(p, next, gn, lane, h);
-  wave_sync_lds();
-
-  // ---- prefix sums: lane-local exclusive prefixes in place, block bases ----
-  lds_u32* blk = S + (uint32_t)lane * M;
-  const bool inblk = (uint32_t)lane * M <= npc;  // (blocks past npc: never queried, not in S)
-  uint32_t run = 0;
-#pragma clang loop unroll(disable)
-  for (uint32_t j = 0; inblk && j < M; j += 4u) {
-    const u32x4 v = *reinterpret_cast<lds_u32x4*>(blk + j);
-    u32x4 e;
-    e.x = run;
-    run = add1c(run, v.x);
-    e.y = run;
-    run = add1c(run, v.y);
-    e.z = run;
-    run = add1c(run, v.z);
-    e.w = run;
-    run = add1c(run, v.w);
-    *reinterpret_cast<lds_u32x4*>(blk + j) = e;
-  }
-  uint32_t incl = run;
-#pragma unroll
-  for (int k = 1; k < 64; k <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)incl, k);
-    if (lane >= k) incl = add1c(incl, t);
-  }
-  const uint32_t excl = (uint32_t)__shfl_up((int)incl, 1);
-  Bs[lane] = lane == 0 ? 0u : excl;
-  wave_sync_lds();
-
-  // ---- the records ----
-  if (valid) {
-    uint32_t res = r4;
-    if (strm) {
-      // P(k) = Bs[k / M] + S[k]; k / M exactly from a float reciprocal
-      // ((k + 0.5) / M is >= 0.5 / M from an integer, k <= 64 M)
-      const float rcp = __builtin_amdgcn_rcpf((float)M);
-      const uint32_t kx = x >> 4, ky = y >> 4;
-      const uint32_t Px = add1c(add1c(Bs[(uint32_t)(((float)kx + 0.5f) * rcp)], S[kx]), px);
-      const u32x4 vm = mask_piece(ve, (int)(y & 15u));
-      const uint32_t Py = add1c(add1c(Bs[(uint32_t)(((float)ky + 0.5f) * rcp)], S[ky]), piece1c(vm));
-      uint32_t tail = add1c(Py, ~Px);
-      // an ICMP segment whose in-prefix bytes are all zero: the difference
-      // cannot tell an all-zero tail (residual 0xffff) from a non-zero one
-      // that sums to zero; the exact sum, serially (rare)
-      if (kind == 2u && acc32 == 0u) tail = span_sum(p, off, (uint32_t)kStreamBase, seg_end);
-      res = (~fold16(add1c(acc32, tail))) & 0xffffu;
-    }
-    store_record(p, i, (!strm || res == 0u) ? rok : rbad, ip_res, res);
-  }
-  // (every lane has read S and Bs before the next chunk writes them)
-  wave_sync_lds();
-}
-
-template <bool OFFS>
-DEV void flat_body(const KParams& p) {
-  constexpr int W = kFlatWaves;
-  __shared__ uint64_t T[12 * 256];
-  __shared__ uint32_t sh_q[W][64], sh_b[W][64];
-  // dynamic LDS: [the IPv6 tables (IXG_TAB6_WORDS, when p.tab6)] then W
-  // arrays of p.flat_cap piece sums
-  extern __shared__ u32x4 dyn6[];
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nw = gridDim.x * W;
-  const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t mode = launch_mode(p);
-  // IXG_MODE_LONG: every chunk, each flagged 0 (done here) or IXG_CLS_LONG;
-  // present[5] tells the general kernel to take only the flagged ones
-  const bool all = mode == IXG_MODE_LONG;
-  if (all) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) p.present[5] = p.epoch;
-  } else if (p.present[IXG_CLS_LONG] != p.epoch) {
-    return;  // nothing deferred long
-  }
-  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_LONG; };
-  const uint32_t wv = blockIdx.x * W + wave;
-  bool any = all;
-  for (uint32_t g = 0; !any && wv + 64u * g * nw < nchunks; g++) {
-    const uint32_t ci = wv + (64u * g + (uint32_t)lane) * nw;
-    any = wave_any(ci < nchunks && mine(ci));
-  }
-  if (!__syncthreads_or(any)) return;
-  const uint32_t t6w = p.tab6 ? IXG_TAB6_WORDS : 0u;
-  if (p.tab6) {
-    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * W)
-      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
-  }
-  stage_tables(p, T);
-  const Tab64 tab{T};
-  const lds_u32* t6 = LDS(const lds_u32, dyn6);
-  lds_u32* S = LDS(lds_u32, dyn6) + t6w + (uint32_t)wave * p.flat_cap;
-  lds_u32* Bs = LDS(lds_u32, sh_b[wave]);
-  lds_u32* q = LDS(lds_u32, sh_q[wave]);
-  bool seen = false;
-  // chunks wv, wv + nw, wv + 2 nw, ... (the grid reads one window of the batch)
-  for (uint32_t g0 = 0; wv + 64u * g0 * nw < nchunks; g0++) {
-    const uint32_t ci = wv + (64u * g0 + (uint32_t)lane) * nw;
-    const bool want = ci < nchunks && (all || mine(ci));
-    const uint64_t m = __ballot(want);
-    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
-    const uint32_t nq = (uint32_t)__popcll(m);
-    __builtin_amdgcn_wave_barrier();
-    if (nq == 0) continue;
-    GDesc D0, D1;
-    gen_desc<OFFS>(p, q[0], lane, D0);
-    const uint32_t c1 = nq > 1 ? q[1] : kNoChunk;
-    gen_desc<OFFS>(p, c1, lane, D1);
-    FlatHead H;
-    flat_head<OFFS>(p, q[0], D0, lane, H);
-    for (uint32_t j = 0; j < nq; j++) {
-      const uint32_t c = H.chunk, cn = j + 1 < nq ? q[j + 1] : kNoChunk;
-      GDesc D2;
-      gen_desc<OFFS>(p, j + 2 < nq ? q[j + 2] : kNoChunk, lane, D2);
-      const bool done = H.ok;
-      if (lane == 0) p.defer[c] = done ? (uint8_t)0 : (uint8_t)IXG_CLS_LONG;
-      seen |= !done;
-      if (done)
-        flat_chunk<OFFS>(p, tab, t6, S, Bs, lane, H, cn, D1);
-      else
-        flat_head<OFFS>(p, cn, D1, lane, H);
-      D1 = D2;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
-}
-
-extern "C" __global__ void __launch_bounds__(64 * kFlatWaves) __attribute__((amdgpu_waves_per_eu(4)))
-ixg_rx_flat_s(KParams p) { flat_body<false>(p); }
-extern "C" __global__ void __launch_bounds__(64 * kFlatWaves) __attribute__((amdgpu_waves_per_eu(4)))
-ixg_rx_flat_o(KParams p) { flat_body<true>(p); }
-#endif  // IXGRX_AB (flat kernel)
-
-#ifdef IXGRX_AB
-IXG_SPAN_KERNEL(ixg_rx_short_spnt_s, false, false, 0, false)
-IXG_SPAN_KERNEL(ixg_rx_short_spnt_o, true, false, 0, false)
-#endif
-#ifdef IXGRX_AB
-// ---- the span-staged short kernel with cross-wave family compaction -------
-// A/B builds only (short variant 1): correct (the GPU suite passes with it
-// as the default) but slower than short_span_body: C5 0.548 vs 0.449 ms,
-// C5 reference semantics 0.506 vs 0.420, C5 in single-family runs 0.872 vs
-// 0.451 in a same-process A/B. The block barriers line the 16 waves up in
-// the same phase, so a step's copies, LDS traffic and parse no longer
-// overlap across waves, which costs more than the specialised parse saves.
-// C5's chunks mix IPv4 (with options) and IPv6 frames in every wave, so every
-// wave ran both the IPv4 header-length mux and hash and the IPv6 Toeplitz.
-// Here the 16 waves of a block each stage one chunk's span in LDS (as
-// short_span_body), then the block's frames are regrouped by header family
-// through LDS: IPv4 / non-IP frames take slots from 0 up, IPv6 frames
-// (IXG_F_IPV6) from 1023 down (one LDS atomic per wave and family), and wave
-// w parses slots [64 w, 64 w + 64) out of the spans of whichever waves hold
-// them. Every wave but the one at the boundary of a full block is then
-// single-family and takes the specialised parse (parse_dispatch). Records go
-// to the frames' own indices. A chunk that is not span-contiguous is parsed
-// by its own wave from per-lane loads. Three block barriers per step: slots
-// taken, spans read (then each wave issues its next chunk's copy), and the
-// step's parse overlaps those copies.
-template <bool OFFS, bool DMX>
-DEV void short_span_cx_body(const KParams& p) {
-  constexpr int W = kSpanWaves;
-  constexpr uint32_t kBuf = kSpanMax / 4 + 32;  // dwords per wave's span buffer
-  __shared__ uint64_t T[12 * 256];
-  __shared__ uint32_t sh_span[W][kBuf];
-  __shared__ uint32_t sh_q[W][64];
-  __shared__ uint32_t sh_desc[W * 64];  // per (wave, lane): dword index into sh_span | L << 16
-  __shared__ uint16_t sh_perm[W * 64];  // slot -> wave * 64 + lane
-  __shared__ uint32_t sh_chunk[W];      // each wave's chunk in this step
-  __shared__ uint32_t sh_nq[W];
-  __shared__ uint32_t sh_cnt[2][2];     // per step parity: IPv4 slots, IPv6 slots taken
-  extern __shared__ u32x4 dyn6[];       // IPv6 Toeplitz tables (IXG_F_IPV6)
-  static_assert(W * kBuf < 65536u, "span dword indices fit 16 bits");
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nw = gridDim.x * W;
-  const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t mode = launch_mode(p);
-  const bool all = mode == IXG_MODE_SHORT;
-  if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
-  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
-  const uint32_t wv = blockIdx.x * W + wave, wv0 = blockIdx.x * W;
-  bool any = all;
-  for (uint32_t g = 0; !any && wv + 64u * g * nw < nchunks; g++) {
-    const uint32_t ci = wv + (64u * g + (uint32_t)lane) * nw;
-    any = wave_any(ci < nchunks && mine(ci));
-  }
-  if (!__syncthreads_or(any)) return;
-  if (p.tab6) {
-    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * W)
-      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
-  }
-  if (threadIdx.x < 4) sh_cnt[threadIdx.x >> 1][threadIdx.x & 1] = 0;
-  stage_tables(p, T);  // (ends with a block barrier)
-  const Tab64 tab{T};
-  const lds_u32* t6 = LDS(const lds_u32, dyn6);
-  lds_u32* buf = LDS(lds_u32, sh_span[wave]);
-  const lds_u32* spans = LDS(const lds_u32, &sh_span[0][0]);
-  lds_u32* q = LDS(lds_u32, sh_q[wave]);
-  bool seen = false;
-  uint32_t step = 0;
-  // chunk assignment as short_span_body (STRIDED); the loop bounds are the
-  // block's, every wave takes part in every barrier
-  for (uint32_t g0 = 0; wv0 + 64u * g0 * nw < nchunks; g0++) {
-    const uint32_t ci = wv + (64u * g0 + (uint32_t)lane) * nw;
-    const bool want = ci < nchunks && (all || mine(ci));
-    const uint64_t m = __ballot(want);
-    if (want) q[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
-    const uint32_t nq = (uint32_t)__popcll(m);
-    if (lane == 0) sh_nq[wave] = nq;
-    __syncthreads();
-    uint32_t nmax = 0;
-#pragma unroll
-    for (int w = 0; w < W; w++) nmax = sh_nq[w] > nmax ? sh_nq[w] : nmax;
-    __syncthreads();  // (sh_nq is rewritten by the next group)
-    if (nmax == 0) continue;
-    auto classify = [&](uint32_t chunk, GDesc& g) {
-      const bool defer = !wave_all(g.L < IXG_SHORT_MAX);  // (L = 0 past the batch end)
-      if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
-      seen |= defer;
-      if (defer) g.L = 0;
-      return !defer;
-    };
-    // a chunk whose frames are not one span of at most kSpanMax bytes goes
-    // to the long kernel (it takes any chunk)
-    auto stage = [&](uint32_t chunk, const GDesc& g, bool& live) {
-      const Span sp = span_issue<OFFS>(p, g, lane, live, buf);
-      if (live && sp.npc == 0u) {
-        if (lane == 0) p.defer[chunk] = (uint8_t)IXG_CLS_LONG;
-        seen = true;
-        live = false;
-      }
-      return sp;
-    };
-    uint32_t c0 = nq > 0 ? q[0] : kNoChunk;
-    GDesc D0, D1;
-    gen_desc<OFFS>(p, c0, lane, D0);
-    bool live0 = nq > 0 && classify(c0, D0);
-    Span S0 = stage(c0, D0, live0);
-    for (uint32_t j = 0; j < nmax; j++, step++) {
-      const uint32_t par = step & 1u;
-      // the next chunk's descriptors (needed after the second barrier)
-      const uint32_t c1 = j + 1 < nq ? q[j + 1] : kNoChunk;
-      gen_desc<OFFS>(p, c1, lane, D1);
-      // ---- this wave's chunk: its frames into the block's slots
-      const uint32_t i = c0 * 64u + (uint32_t)lane;
-      const bool valid = live0 && i < p.n;
-      const bool staged = S0.npc != 0;  // wave-uniform
-      const uint32_t L = D0.L;
-      uint32_t fam = 2u, w0 = 0u;  // 0: IPv4 / other, 1: IPv6, 2: not here
-      if (staged) {
-        __builtin_amdgcn_s_waitcnt(kGldsWait);
-        __builtin_amdgcn_wave_barrier();
-        w0 = (uint32_t)(D0.off - S0.base) >> 2;
-        const uint32_t dw3 = buf[L ? w0 + 3u : 0u];  // bytes 12..15
-        const uint32_t et = ((L > 12u ? dw3 & 0xffu : 0u) << 8) | (L > 13u ? (dw3 >> 8) & 0xffu : 0u);
-        fam = !valid ? 2u : (((p.flags & IXG_F_IPV6) && et == 0x86DDu) ? 1u : 0u);
-      }
-      const uint64_t b4 = __ballot(fam == 0u), b6 = __ballot(fam == 1u);
-      uint32_t base4 = 0, base6 = 0;
-      if (lane == 0) {
-        if (b4) base4 = atomicAdd(&sh_cnt[par][0], (uint32_t)__popcll(b4));
-        if (b6) base6 = atomicAdd(&sh_cnt[par][1], (uint32_t)__popcll(b6));
-      }
-      base4 = __builtin_amdgcn_readfirstlane(base4);
-      base6 = __builtin_amdgcn_readfirstlane(base6);
-      if (fam < 2u) {
-        const uint64_t bm = fam == 0u ? b4 : b6;
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-        const uint32_t slot = fam == 0u ? base4 + r : (uint32_t)(W * 64 - 1) - (base6 + r);
-        sh_perm[slot] = (uint16_t)(wave * 64 + lane);
-      }
-      sh_desc[wave * 64 + lane] = ((uint32_t)wave * kBuf + w0) | (L << 16);
-      if (lane == 0) sh_chunk[wave] = c0;
-      __syncthreads();  // slots taken
-      const uint32_t n4 = sh_cnt[par][0], n6 = sh_cnt[par][1];
-      if (wave == 0 && lane < 2) sh_cnt[par ^ 1u][lane] = 0;  // the next step's (last read before this step)
-      // ---- slots [64 wave, 64 wave + 64): read the frames' prefixes
-      const uint32_t sl = (uint32_t)(wave * 64 + lane);
-      const bool have = sl < n4 || sl >= (uint32_t)(W * 64) - n6;
-      const uint32_t pd = have ? (uint32_t)sh_perm[sl] : 0u;
-      const uint32_t de = sh_desc[pd];
-      const uint32_t Ls = have ? de >> 16 : 0u;
-      const uint32_t is = sh_chunk[pd >> 6] * 64u + (pd & 63u);
-      uint32_t d[kPrefixDw];
-      u32x4 v96 = {0u, 0u, 0u, 0u};
-      {
-        const lds_u32* f = spans + (have ? (de & 0xffffu) : 0u);
-        d[0] = d[1] = d[2] = 0;
-#pragma unroll
-        for (int k = 3; k < kPrefixDw; k++) d[k] = f[k];
-        if (wave_any(Ls > (uint32_t)kStreamBase)) v96 = u32x4{f[24], f[25], f[26], f[27]};
-      }
-      __builtin_amdgcn_s_waitcnt(kLdsWait);
-      __syncthreads();  // every span read: the buffers may be refilled
-      bool live1 = false;
-      Span S1{0, 0};
-      if (j + 1 < nq) {
-        live1 = classify(c1, D1);
-        S1 = stage(c1, D1, live1);
-      }
-      // ---- parse the slots (single-family waves but at a full block's boundary)
-      if (wave_any(have)) {
-        LaneState st;
-        parse_dispatch(p, tab, d, Ls, have, st, t6);
-        if (have && st.stream) st.l4_acc += piece_sum(v96, (int)(st.seg_end - (uint32_t)kStreamBase));
-        if (have) {
-          const uint32_t r4 = l4_residual(st);
-          const Rec r = make_record(p, d, Ls, st, r4);
-          store_record(p, is, r, st.ip_res, r4);
-          store_demux<DMX>(p, is, r, st.src, st.dst, st.ports);
-        }
-      }
-      c0 = c1;
-      D0 = D1;
-      live0 = live1;
-      S0 = S1;
-    }
-  }
-  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
-}
-
-#define IXG_SPANCX_KERNEL(NAME, OFFS, DMX)                                                                     \
-  extern "C" __global__ void __launch_bounds__(64 * kSpanWaves) __attribute__((amdgpu_waves_per_eu(4))) \
-  NAME(KParams p) { short_span_cx_body<OFFS, DMX>(p); }
-IXG_SPANCX_KERNEL(ixg_rx_short_spx_s, false, false)
-IXG_SPANCX_KERNEL(ixg_rx_short_spx_o, true, false)
-#endif
-
-#ifdef IXGRX_AB
-IXG_GENW_KERNEL(ixg_rx_short_w10_s, 10, false, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
-IXG_GENW_KERNEL(ixg_rx_short_w10_o, 10, true, IXG_CLS_SHORT, 5, false, 0, false, true, 10, 4, false)
-#endif
-#ifdef IXGRX_AB
-IXG_GEN_KERNEL(ixg_rx_short_late_s, false, IXG_CLS_SHORT, 4, false)
-IXG_GEN_KERNEL(ixg_rx_short_late_o, true, IXG_CLS_SHORT, 4, false)
-#endif
-
-// ---- the compacted short kernel (wavefront compaction across waves) ------
-// A block of kCxWaves waves takes a tile of kCxWaves short chunks (one per
-// wave) at a time. Phase 1: each lane loads its frame's prefix and classes
-// it: A = IPv4 ihl 5, C = other IPv4, B = IPv6 under IXG_F_IPV6, D = no IP
-// parse at all (ARP, other ethertypes, IPv6 in the reference's semantics:
-// ip.c:132-137), whose record is a constant of the ethertype and L and is
-// written at once. The A, C and B lanes are ranked by class across the
-// tile's waves (ballot + mbcnt + per-wave counts) and their prefixes written
-// to LDS in that order. Phase 2: the waves take the ranked list 64 entries at
-// a time, so nearly every wave holds one family and runs the parse
-// specialised for it (constant geometry for ihl 5 and for IPv6, no IPv6
-// code for IPv4). Only the waves straddling a class boundary run the
-// general parse. Records go to their frames' slots directly.
-constexpr int kCxWaves = 8;
-constexpr int kCxDw = 25;  // per ranked entry: bytes 16..111 (24 dwords) + meta
-constexpr uint32_t kClsA = 0, kClsC = 1, kClsB = 2, kClsD = 3, kClsNone = 4;
-
-struct __attribute__((aligned(16))) CxLds {
-  uint32_t t32[12 * 256];   // Toeplitz byte tables
-  uint16_t t16[12 * 256];   // CRC-32C byte tables (low 16 bits)
-  uint32_t x[kCxWaves * 64 * kCxDw];  // ranked prefixes
-  uint32_t cl[kCxWaves * 64];         // the block group's chunk list
-  uint32_t cnt[kCxWaves][4];          // per-wave counts (A, C, B; list fill)
-};
-
-// The record of a frame that eth_input never hands to ip_input: ARP
-// (ip.c:134-135) or a dropped ethertype (ip.c:136-137). No checksum is
-// checked, no RSS (fg = the device's group 0), no bucket.
-DEV Rec trivial_record(const KParams& p, uint32_t etype, uint32_t L) {
-  const bool arp = etype == 0x0806u;
-  Rec r;
-  r.w0 = p.fg_base | ((arp ? (uint32_t)IXG_V_ARP : (uint32_t)IXG_V_DROP_ETHERTYPE) << 16);
-  r.w1 = arp ? (14u | (((L >= 14 ? L - 14 : 0u) & 0xffffu) << 16)) : 0u;
-  r.w2 = 0;
-  r.w3 = IXG_NO_BUCKET;
-  return r;
-}
-
-// One ranked entry, parsed with the wave's shape: prefix from LDS, parse,
-// record, stores. A function per shape, called from a wave-uniform branch,
-// each reading its own copy of the entry (shared code hoisted above the
-// branch would stay live through every shape).
-template <int SHAPE>
-DEV void cx_entry(const KParams& p, const TabSplit& T, const lds_u32* t6, const lds_u32* e, uint32_t c2, bool ok,
-                  const lds_u32* CL, uint32_t t) {
-  uint32_t dd[kPrefixDw];
-  const uint32_t meta = e[24];
-  // bytes 12..13 (the ethertype) follow from the class
-  dd[0] = dd[1] = dd[2] = 0;
-  dd[3] = (c2 == kClsB ? 0xDD86u : 0x0008u) | (meta << 16);
-#pragma unroll
-  for (int j = 4; j < kPrefixDw; j++) dd[j] = e[j - 4];
-  const uint32_t Lx = (meta >> 16) & 0x7fu;
-  LaneState st;
-  lane_parse<SHAPE, kPrefixDw>(p, T, dd, Lx, st, t6);
-  // the 16-byte piece holding a segment end past byte 96 (frames < 112 B)
-  // and the frame's index, read only now (fewer registers live in the parse)
-  if (st.stream) {
-    const u32x4 v96 = {e[20], e[21], e[22], e[23]};
-    st.l4_acc += piece_sum(v96, (int)(st.seg_end - (uint32_t)kStreamBase));
-  }
-  if (ok) {
-    const uint32_t ti = e[24] >> 23;
-    const uint32_t ix = CL[t + (ti >> 6)] * 64u + (ti & 63u);
-    const uint32_t r4 = l4_residual(st);
-    const Rec r = make_record(p, dd, Lx, st, r4);
-    store_record(p, ix, r, st.ip_res, r4);
-    store_demux(p, ix, r, st.src, st.dst, st.ports);
-  }
-}
-
-// SHAPES: bit k = shape k may be used (A/B of the specialisations)
-template <bool OFFS, int SHAPES = 15>
-DEV void short_cx_body(const KParams& p) {
-  extern __shared__ u32x4 dyn6[];  // IPv6 Toeplitz tables (IXG_F_IPV6)
-  __shared__ CxLds sh;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t nbg = (nchunks + 64u * kCxWaves - 1u) / (64u * kCxWaves);  // block groups
-  const uint32_t mode = launch_mode(p);
-  const bool all = mode == IXG_MODE_SHORT;
-  if (!all && p.present[IXG_CLS_SHORT] != p.epoch) return;  // nothing deferred short
-  auto mine = [&](uint32_t ci) { return p.defer[ci] == IXG_CLS_SHORT; };
-  bool any = all;
-  for (uint32_t g = blockIdx.x * kCxWaves + wave; !any && g < nbg * kCxWaves; g += gridDim.x * kCxWaves) {
-    const uint32_t ci = g * 64u + (uint32_t)lane;
-    any = __ballot(ci < nchunks && mine(ci)) != 0;
-  }
-  if (!__syncthreads_or(any)) return;
-  if (p.tab6) {
-    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kCxWaves)
-      dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
-  }
-  for (int k = threadIdx.x; k < 12 * 256 / 4; k += 64 * kCxWaves)
-    reinterpret_cast<u32x4*>(sh.t32)[k] = reinterpret_cast<const u32x4*>(p.tab32)[k];
-  for (int k = threadIdx.x; k < 12 * 256 / 8; k += 64 * kCxWaves)
-    reinterpret_cast<u32x4*>(sh.t16)[k] = reinterpret_cast<const u32x4*>(p.tab16)[k];
-  __syncthreads();
-  const TabSplit T{LDS(const lds_u32, sh.t32), LDS(const lds_u16, sh.t16)};
-  const lds_u32* t6 = LDS(const lds_u32, dyn6);
-  lds_u32* X = LDS(lds_u32, sh.x);
-  lds_u32* CL = LDS(lds_u32, sh.cl);
-  bool seen = false;
-  for (uint32_t bg = blockIdx.x; bg < nbg; bg += gridDim.x) {
-    // the block group's chunks (kCxWaves x 64), the short ones in order
-    {
-      const uint32_t ci = (bg * kCxWaves + wave) * 64u + (uint32_t)lane;
-      const bool want = ci < nchunks && (all || mine(ci));
-      const uint64_t m = __ballot(want);
-      if (lane == 0) sh.cnt[wave][3] = (uint32_t)__popcll(m);
-      __syncthreads();
-      uint32_t base = 0;
-      for (int w = 0; w < wave; w++) base += sh.cnt[w][3];
-      if (want) CL[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = ci;
-    }
-    __syncthreads();
-    uint32_t nq = 0;
-    for (int w = 0; w < kCxWaves; w++) nq += sh.cnt[w][3];
-    __syncthreads();  // (the counts are rewritten below)
-    for (uint32_t t = 0; t < nq; t += kCxWaves) {
-      // ---- phase 1: this wave's chunk ----
-      const uint32_t tc = t + (uint32_t)wave;
-      const uint32_t chunk = tc < nq ? CL[tc] : kNoChunk;
-      GDesc g;
-      gen_desc<OFFS>(p, chunk, lane, g);
-      bool live = chunk != kNoChunk;
-      if (live) {
-        const bool defer = !wave_all(g.L < IXG_SHORT_MAX);  // (g.L = 0 past the batch end)
-        if (lane == 0) p.defer[chunk] = defer ? (uint8_t)IXG_CLS_LONG : (uint8_t)0;
-        seen |= defer;
-        live = !defer;
-      }
-      if (!live) g.L = 0;  // (no frame bytes for a deferred chunk)
-      GPre x;
-      gen_pre<false, false>(p, g, lane, x);
-      const uint32_t i = chunk * 64u + (uint32_t)lane;
-      const bool valid = live && i < p.n;
-      const uint32_t L = g.L;
-      uint32_t d[kPrefixDw];
-#pragma unroll
-      for (int j = 0; j < kPrefixDw; j++) d[j] = x.d[j];
-      mask_prefix(d, L);
-      const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
-      uint32_t cls = kClsNone;
-      if (valid) {
-        if (etype == 0x0800u) cls = byte_at(d, 14) == 0x45u ? kClsA : kClsC;
-        else if (etype == 0x86DDu && (p.flags & IXG_F_IPV6)) cls = kClsB;
-        else cls = kClsD;
-      }
-      if (cls == kClsD) {
-        const Rec r = trivial_record(p, etype, L);
-        store_record(p, i, r, 0xffffu, 0xffffu);
-        store_demux(p, i, r, 0u, 0u, 0u);
-      }
-      const uint64_t mA = __ballot(cls == kClsA), mC = __ballot(cls == kClsC), mB = __ballot(cls == kClsB);
-      if (lane == 0) {
-        sh.cnt[wave][0] = (uint32_t)__popcll(mA);
-        sh.cnt[wave][1] = (uint32_t)__popcll(mC);
-        sh.cnt[wave][2] = (uint32_t)__popcll(mB);
-      }
-      __syncthreads();
-      uint32_t tot[3] = {0, 0, 0}, before[3] = {0, 0, 0};
-#pragma unroll
-      for (int w = 0; w < kCxWaves; w++) {
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-          const uint32_t c = sh.cnt[w][k];
-          tot[k] += c;
-          before[k] += w < wave ? c : 0u;
-        }
-      }
-      if (cls < kClsD) {
-        const uint64_t mm = cls == kClsA ? mA : (cls == kClsC ? mC : mB);
-        const uint32_t cbase = cls == kClsA ? 0u : (cls == kClsC ? tot[0] : tot[0] + tot[1]);
-        const uint32_t pos = cbase + (cls == kClsA ? before[0] : (cls == kClsC ? before[1] : before[2])) +
-                             __builtin_amdgcn_mbcnt_hi((uint32_t)(mm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mm, 0u));
-        lds_u32* e = X + pos * kCxDw;
-#pragma unroll
-        for (int j = 4; j < kPrefixDw; j++) e[j - 4] = d[j];
-        e[20] = x.v96.x; e[21] = x.v96.y; e[22] = x.v96.z; e[23] = x.v96.w;
-        e[24] = (d[3] >> 16) | (L << 16) | ((uint32_t)(wave * 64 + lane) << 23);
-      }
-      __syncthreads();
-      // ---- phase 2: the ranked entries, 64 per wave ----
-      const uint32_t nA = tot[0], nAC = tot[0] + tot[1], nit = nAC + tot[2];
-      for (uint32_t k = (uint32_t)wave; 64u * k < nit; k += kCxWaves) {
-        const uint32_t pos = 64u * k + (uint32_t)lane;
-        const bool ok = pos < nit;
-        const lds_u32* e = X + (ok ? pos : 0u) * kCxDw;
-        const uint32_t c2 = pos < nA ? kClsA : (pos < nAC ? kClsC : kClsB);
-        const bool allA = wave_all(!ok || c2 == kClsA), allAC = wave_all(!ok || c2 != kClsB),
-                   allB = wave_all(!ok || c2 == kClsB);
-        if ((SHAPES & 1) && allA)
-          cx_entry<kShapeFixed>(p, T, t6, e, c2, ok, CL, t);
-        else if ((SHAPES & 2) && allAC)
-          cx_entry<kShapeV4>(p, T, t6, e, c2, ok, CL, t);
-        else if ((SHAPES & 4) && allB)
-          cx_entry<kShapeV6>(p, T, t6, e, c2, ok, CL, t);
-        else
-          cx_entry<kShapeAny>(p, T, t6, e, c2, ok, CL, t);
-      }
-      __syncthreads();  // X and the counts are reused by the next tile
-    }
-  }
-  publish_classes(p, seen ? 1u << IXG_CLS_LONG : 0u, lane);
-}
-
-#define IXG_CX_KERNEL(NAME, OFFS, ...)                                                                      \
-  extern "C" __global__ void __launch_bounds__(64 * kCxWaves) __attribute__((amdgpu_waves_per_eu(4))) \
-  NAME(KParams p) { short_cx_body<OFFS, ##__VA_ARGS__>(p); }
-#ifdef IXGRX_AB
-IXG_CX_KERNEL(ixg_rx_short_cx_s, false)
-IXG_CX_KERNEL(ixg_rx_short_cx_o, true)
-IXG_CX_KERNEL(ixg_rx_short_cx6_s, false, 4)
-IXG_CX_KERNEL(ixg_rx_short_cx6_o, true, 4)
-IXG_CX_KERNEL(ixg_rx_short_cx46_s, false, 6)
-IXG_CX_KERNEL(ixg_rx_short_cx46_o, true, 6)
-IXG_CX_KERNEL(ixg_rx_short_cx0_s, false, 0)
-IXG_CX_KERNEL(ixg_rx_short_cx0_o, true, 0)
-#endif
-#ifdef IXGRX_AB
-// A/B builds only (IXGRX_GEN_VARIANT / IXGRX_SHORT_VARIANT)
-// round 1's second dispatch behind the coalesced kernel (both classes); the
-// coalesced kernel now finishes its deferred chunks itself
-IXG_GEN_KERNEL(ixg_rx_any_s, false, IXG_CLS_ANY, 2)
-IXG_GEN_KERNEL(ixg_rx_general_w3_s, false, IXG_CLS_LONG, 3)
-IXG_GEN_KERNEL(ixg_rx_general_w3_o, true, IXG_CLS_LONG, 3)
-IXG_GEN_KERNEL(ixg_rx_general_w4_s, false, IXG_CLS_LONG, 4)
-IXG_GEN_KERNEL(ixg_rx_general_w4_o, true, IXG_CLS_LONG, 4)
-// every long segment streamed by 16-lane groups (the split's A/B baseline)
-IXG_GEN_KERNEL(ixg_rx_general_g16_s, false, IXG_CLS_LONG, 2)
-IXG_GEN_KERNEL(ixg_rx_general_g16_o, true, IXG_CLS_LONG, 2)
-// LATE: the next prefix loaded behind the last streaming round (C3 -1.2%
-// time but FETCH_SIZE +10%: 6.53 -> 7.18 GB per launch; not the default)
-IXG_GEN_KERNEL(ixg_rx_general_lt_s, false, IXG_CLS_LONG, 2, true, 1, true)
-IXG_GEN_KERNEL(ixg_rx_general_lt_o, true, IXG_CLS_LONG, 2, true, 1, true)
-// packed stream mapping (SM 2)
-IXG_GEN_KERNEL(ixg_rx_general_pk_s, false, IXG_CLS_LONG, 2, true, 2)
-IXG_GEN_KERNEL(ixg_rx_general_pk_o, true, IXG_CLS_LONG, 2, true, 2)
-IXG_GEN_KERNEL(ixg_rx_short_s, false, IXG_CLS_SHORT, 3)
-IXG_GEN_KERNEL(ixg_rx_short_o, true, IXG_CLS_SHORT, 3)
-IXG_GEN_KERNEL(ixg_rx_short_w4_s, false, IXG_CLS_SHORT, 4)
-IXG_GEN_KERNEL(ixg_rx_short_w4_o, true, IXG_CLS_SHORT, 4)
-// no big-chunk path, no one-ahead prefix: 3 waves/SIMD
-IXG_GEN_KERNEL(ixg_rx_general_w3nb_s, false, IXG_CLS_LONG, 3, false, 1, false, false)
-IXG_GEN_KERNEL(ixg_rx_general_w3nb_o, true, IXG_CLS_LONG, 3, false, 1, false, false)
-#endif
 
 // The sampler: one block picks the launch's IXG_MODE_*: FAST when at least
 // half of the sampled chunks could be fixed-shape by length (every frame <=
@@ -3004,61 +2158,17 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_sample(KParams p) {
 }
 
 typedef void (*kern_fn)(KParams);
-#ifdef IXGRX_AB
-// LDS per workgroup (gfx950); the flat kernel's dynamic part is this less
-// its static arrays (hash tables, per-wave chunk queues and block bases)
-constexpr size_t kLdsMax = 160u * 1024u;
-// variant bit 30: the flat long kernel (A/B builds)
-constexpr int kFlatOn = 1 << 30;
-#endif
-// [variant][layout: 0 = stride, 1 = offsets]; the product library has only
-// variant 0 (the default kernels)
-static const kern_fn k_fast[][2] = {{ixg_rx_fast_s, ixg_rx_fast_o}
-#ifdef IXGRX_AB
-                                    , {ixg_rx_fast_a2w4_s, ixg_rx_fast_a2w4_o},
-                                    {ixg_rx_fast_a2w5_s, ixg_rx_fast_a2w5_o},
-                                    {ixg_rx_fast_a1w4_s, ixg_rx_fast_a1w4_o}
-#endif
-};
-static const kern_fn k_gen[][2] = {{ixg_rx_general_s, ixg_rx_general_o}
-#ifdef IXGRX_AB
-                                   , {ixg_rx_general_w3_s, ixg_rx_general_w3_o},
-                                   {ixg_rx_general_w4_s, ixg_rx_general_w4_o},
-                                   {ixg_rx_general_g16_s, ixg_rx_general_g16_o},
-                                   {ixg_rx_general_pk_s, ixg_rx_general_pk_o},
-                                   {ixg_rx_general_lt_s, ixg_rx_general_lt_o},
-                                   {ixg_rx_general_w3nb_s, ixg_rx_general_w3nb_o}
-#endif
-};
-// the short kernel (512-thread blocks by default)
+// [layout: 0 = stride, 1 = offsets]
+static const kern_fn k_fast[2] = {ixg_rx_fast_s, ixg_rx_fast_o};
+static const kern_fn k_gen[2] = {ixg_rx_general_s, ixg_rx_general_o};
+// the short kernel and its block size: the span-staged kernel, or with the
+// fused demux (p.dmx) the general short kernel in 512-thread blocks
 struct ShortK {
   kern_fn k[2];
   int block;
 };
-// with the fused demux (p.dmx)
 static const ShortK k_short_dmx = {{ixg_rx_short_w8d_s, ixg_rx_short_w8d_o}, 512};
-static const ShortK k_short[] = {{{ixg_rx_short_sp_s, ixg_rx_short_sp_o}, 64 * kSpanWaves}
-#ifdef IXGRX_AB
-                                 , {{ixg_rx_short_spx_s, ixg_rx_short_spx_o}, 64 * kSpanWaves}
-                                 , {{ixg_rx_short_w8_s, ixg_rx_short_w8_o}, 512},
-                                 {{ixg_rx_short_spnt_s, ixg_rx_short_spnt_o}, 64 * kSpanWaves}
-                                 , {{ixg_rx_short_w10_s, ixg_rx_short_w10_o}, 640}
-                                 , {{ixg_rx_short_late_s, ixg_rx_short_late_o}, kBlock},
-                                 {{ixg_rx_short_w4_s, ixg_rx_short_w4_o}, kBlock},
-                                 {{ixg_rx_short_s, ixg_rx_short_o}, kBlock},
-                                 {{ixg_rx_short_cx_s, ixg_rx_short_cx_o}, 64 * kCxWaves},
-                                 {{ixg_rx_short_cx6_s, ixg_rx_short_cx6_o}, 64 * kCxWaves},
-                                 {{ixg_rx_short_cx0_s, ixg_rx_short_cx0_o}, 64 * kCxWaves}
-#endif
-};
-#ifdef IXGRX_AB
-// the parse kernel of the parse / tail split (A/B builds only)
-static const kern_fn k_parse[][2] = {{ixg_rx_parse_s, ixg_rx_parse_o}, {ixg_rx_parse4_s, ixg_rx_parse4_o}};
-static const int k_nparse = sizeof(k_parse) / sizeof(k_parse[0]);
-#endif
-static const int k_nshort = sizeof(k_short) / sizeof(k_short[0]);
-static const int k_nfast = sizeof(k_fast) / sizeof(k_fast[0]);
-static const int k_ngen = sizeof(k_gen) / sizeof(k_gen[0]);
+static const ShortK k_short = {{ixg_rx_short_sp_s, ixg_rx_short_sp_o}, 64 * kSpanWaves};
 
 // blocks per CU, cached per (kernel, dynamic LDS): a handful of entries,
 // filled under a lock (contexts on several host threads launch concurrently)
@@ -3082,26 +2192,14 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
   return g ? (uint32_t)g : 1u;
 }
 
-// variant = fast_variant | (general_variant << 8) | (short_variant << 16). Fast variant 0 picks the
-// coalesced kernel for fixed strides <= 64 B (16-B aligned base), else the
-// lane-load kernel; 1..3 force the lane-load A/B builds; 4 forces variant
-// 0's lane-load kernel.
-extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void* stream) {
+// The launch plan: coalesced fixed strides <= 64 B
+// (16-B aligned base) take the coalesced fixed-shape kernel alone; other
+// layouts the span-staged short kernel, which samples the mode itself, then
+// the general kernel for what it deferred. Forced splits (ixg_rx_set_split,
+// tests) and the fused demux run the sampler and the lane-load fixed-shape
+// kernel first.
+extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
-  int fv = variant & 0xff, gv = (variant >> 8) & 0xff, sv = (variant >> 16) & 0xff;
-#ifdef IXGRX_AB
-  // A/B builds: general variant 20 + k = the parse / tail split with parse
-  // variant k (with the defer flags)
-  bool split = false;
-  int pv = 0;
-  if (gv >= 20) {
-    split = true;
-    pv = gv - 20 < k_nparse ? gv - 20 : 0;
-    gv = 0;
-  }
-#endif
-  if (gv >= k_ngen) gv = 0;
-  if (sv >= k_nshort) sv = 0;
   const int lay = p.off ? 1 : 0;
   const uint64_t nchunks = ((uint64_t)p.n + 63u) / 64u;
   const uint64_t wave_blocks = (nchunks + kWaves - 1) / kWaves;              // one wave per chunk
@@ -3111,22 +2209,20 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   const size_t sh6 = p.tab6 ? IXG_TAB6_WORDS * sizeof(uint32_t) : 0u;
   // offset and wide-stride batches in the default split: the span-staged
   // short kernel runs first and samples the mode itself (no sampler, no
-  // fixed-shape kernel dispatch); forced splits, the fused demux and the A/B
-  // variants keep the sampler + fixed-shape kernel plan
-  const bool self = p.defer && !coal && fv == 0 && sv == 0 && !p.dmx && p.force_mode == IXG_MODE_AUTO;
+  // fixed-shape kernel dispatch); forced splits and the fused demux keep the
+  // sampler + fixed-shape kernel plan
+  const bool self = p.defer && !coal && !p.dmx && p.force_mode == IXG_MODE_AUTO;
   if (p.defer && !self) {
     kern_fn kf = nullptr;
     const bool forced = p.force_mode != IXG_MODE_AUTO;
-    if (fv == 0 && coal) {
+    if (coal) {
       // coalesced fixed stride: always fixed-shape first (no sampler),
       // unless a test forces another split
       if (forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
       if (!forced || p.force_mode == IXG_MODE_FAST) kf = p.dmx ? ixg_rx_fastc_dmx_s : ixg_rx_fastc_s;
     } else {
-      // fast variant 5: no sampler (the fixed-shape kernel always runs first)
-      if (fv != 5 || forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
-      if (fv >= k_nfast) fv = 0;
-      kf = k_fast[fv][lay];
+      hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
+      kf = k_fast[lay];
     }
     // the coalesced kernel runs 8 resident-grids' worth of blocks (each wave
     // ~8 chunks): 3-4% faster on C2 than one persistent grid (A/B of 1x, 2x,
@@ -3146,11 +2242,10 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
   }
   // coalesced batches in the default split: the coalesced kernel finished
   // every chunk itself
-  if (p.defer && fv == 0 && coal && p.force_mode == IXG_MODE_AUTO && gv == 0) return (int)hipGetLastError();
+  if (p.defer && coal && p.force_mode == IXG_MODE_AUTO) return (int)hipGetLastError();
   if (p.defer) {
-    const ShortK& ks = p.dmx ? k_short_dmx : k_short[sv];
-    // the general kernels: one wave per 64 chunks; the compacted A/B build:
-    // one block per 64 chunks per wave
+    const ShortK& ks = p.dmx ? k_short_dmx : k_short;
+    // one wave per 64 chunks (frames in host memory: one per chunk)
     const uint64_t ngroups = (nchunks + 63u) / 64u, bw = (uint64_t)ks.block / 64u;
     const uint64_t want = ((p.host_mem ? nchunks : ngroups) + bw - 1) / bw;
     KParams ps = p;
@@ -3158,46 +2253,7 @@ extern "C" int ixgrx_launch(const void* params, int variant, uint32_t ncu, void*
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
                        (hipStream_t)stream, ps);
   }
-#ifdef IXGRX_AB
-  // the parse / tail split: the parse kernel, then the tail kernel over the
-  // tails it left (exits at once when none)
-  if (split && p.defer && p.tail) {
-    const kern_fn kp = k_parse[pv][lay];
-    hipLaunchKernelGGL(kp, dim3(grid_for(kp, group_blocks, ncu, sh6)), dim3(kBlock), sh6, (hipStream_t)stream, p);
-    hipLaunchKernelGGL(ixg_rx_tail, dim3(grid_for(ixg_rx_tail, group_blocks, ncu)), dim3(kBlock), 0,
-                       (hipStream_t)stream, p);
-    return (int)hipGetLastError();
-  }
-#endif
-  // A/B builds, IXGRX_FLAT=1: the flat long kernel (not with the fused
-  // demux) takes the long chunks whose span fits its LDS, the general kernel
-  // the rest
-#ifdef IXGRX_AB
-  if (p.defer && !p.dmx && gv == 0 && (variant & kFlatOn)) {
-    static std::once_flag once;
-    static size_t dyn_max = 0;
-    std::call_once(once, [] {
-      size_t st = 0;
-      for (kern_fn k : {ixg_rx_flat_s, ixg_rx_flat_o}) {
-        hipFuncAttributes a;
-        if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(k)) == hipSuccess && a.sharedSizeBytes > st)
-          st = a.sharedSizeBytes;
-      }
-      dyn_max = kLdsMax - (st ? st : 40u * 1024u);
-      for (kern_fn k : {ixg_rx_flat_s, ixg_rx_flat_o})
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)dyn_max);
-    });
-    KParams pf = p;
-    pf.flat_cap = (uint32_t)((dyn_max - sh6) / (4u * kFlatWaves)) & ~63u;
-    const size_t dyn = sh6 + (size_t)pf.flat_cap * 4u * kFlatWaves;
-    const kern_fn kfl = lay ? ixg_rx_flat_o : ixg_rx_flat_s;
-    const uint64_t want = ((nchunks + 63u) / 64u + kFlatWaves - 1) / kFlatWaves;
-    hipLaunchKernelGGL(kfl, dim3(grid_for(kfl, want, ncu, dyn, 64 * kFlatWaves)), dim3(64 * kFlatWaves), dyn,
-                       (hipStream_t)stream, pf);
-  }
-#endif
-  const kern_fn kg = k_gen[gv][lay];
+  const kern_fn kg = k_gen[lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, p.host_mem ? wave_blocks : group_blocks, ncu, sh6)), dim3(kBlock), sh6,
                      (hipStream_t)stream, p);
   return (int)hipGetLastError();

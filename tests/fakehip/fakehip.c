@@ -318,9 +318,8 @@ hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int f)
 }
 
 /* ---- the kernels' launch entry points (ixgrx_internal.h) ------------------ */
-int ixgrx_launch(const void *params, int variant, uint32_t ncu, void *stream)
+int ixgrx_launch(const void *params, uint32_t ncu, void *stream)
 {
-	(void)variant;
 	(void)ncu;
 	struct op *o = new_op(OP_RX);
 	memcpy(&o->p, params, sizeof(o->p));

@@ -8,5 +8,5 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=$ROOT/build/rev_$NAME
 rm -rf "$T" && mkdir -p "$T" "$ROOT/tools/ablib"
 git -C "$ROOT" archive "$REV" ix_amd/csrc include examples | tar -x -C "$T"
-make -s -C "$T/ix_amd/csrc" AB=1 OUT="$ROOT/tools/ablib/$NAME.so" OBJ="$T/obj" 2>&1 | grep -v hip-link || true
+make -s -C "$T/ix_amd/csrc" OUT="$ROOT/tools/ablib/$NAME.so" OBJ="$T/obj" 2>&1 | grep -v hip-link || true
 ls -la "$ROOT/tools/ablib/$NAME.so"

@@ -17,5 +17,5 @@ t = eval(expr, {"re": re, "s": s})
 assert t != s, "variant edit changed nothing"
 open(p, "w").write(t)
 PY
-make -s -C "$T/ix_amd/csrc" AB=1 OUT="$ROOT/tools/ablib/$NAME.so" OBJ="$T/obj" 2>&1 | grep -v hip-link || true
+make -s -C "$T/ix_amd/csrc" OUT="$ROOT/tools/ablib/$NAME.so" OBJ="$T/obj" 2>&1 | grep -v hip-link || true
 ls -la "$ROOT/tools/ablib/$NAME.so"
