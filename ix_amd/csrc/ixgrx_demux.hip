@@ -9,9 +9,12 @@
 // mirror of IX's hlists (include/ixgrx.h struct ixg_demux_tables) in HBM;
 // they are small next to a batch and stay in L2 / Infinity Cache.
 //
-// A persistent grid-stride loop over 64-frame chunks; the record and the
-// frame's header bytes of the next chunk are loaded while the current chunk
-// walks its lists (dependent loads: that walk is the latency this hides).
+// A persistent grid-stride loop over 64-frame chunks, three stages deep: the
+// record and header bytes of chunk k+1 are loaded, the bucket lines of chunk
+// k (ixgwalk::lines_issue, 4 lanes per line) are loaded, and the lookups of
+// chunk k-1 are matched (their lines reach their lanes through the wave's
+// LDS), so neither dependent load is waited for in the iteration that issues
+// it.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -61,55 +64,86 @@ DEV void load_item(const DParams& p, uint32_t chunk, int lane, Item& it) {
   it.h1 = *reinterpret_cast<const u32x4_a4*>(f + 28);
 }
 
+// a chunk's lookups in flight: lines loaded, matched an iteration later
+struct Pend {
+  u32x4 piece[4];  // ixgwalk::lines_issue's pieces
+  uint32_t key;    // ixgwalk::lookup_key
+  uint32_t src, dst, ports;
+};
+constexpr uint32_t kNoChunk = 0xffffffffu;
+
+// the record and header bytes of frame i -> its lookup, bucket lines issued
 template <bool OFFS>
-DEV void walk_item(const DParams& p, uint32_t i, const Item& it) {
-  const uint32_t verdict = (it.rec.x >> 16) & 0xffu;
-  uint32_t kind = IXG_D_NONE, id = 0;
-  if (verdict == IXG_V_TCP) {
-    const uint32_t fg = ixg_demux_group(it.rec.x & 0xffffu, p.fg_base, p.nfg, p.n_out);  // fgs[pkt->fg_id]
-    const uint32_t bucket = it.rec.w & 0xffffu;             // tcp_to_idx (tcp_in.c:233)
-    const uint32_t tflags = (it.rec.w >> 16) & 0xffu;
-    const uint32_t ihl = (it.h0.x >> 16) & 15u;             // frame byte 14
-    // src = bytes 26..29, dst = bytes 30..33 (raw, network order as loaded LE)
-    const uint32_t src = (it.h0.w >> 16) | (it.h1.x << 16);
-    const uint32_t dst = (it.h1.x >> 16) | (it.h1.y << 16);
-    uint32_t sw, dw;  // ports: L4 bytes 0..3 at 14 + 4*ihl
-    if (ihl == 5) {
-      sw = it.h1.y >> 16;
-      dw = it.h1.z & 0xffffu;
-    } else {  // IP options: one more (dependent) load, rare
-      const uint8_t* f = p.base + frame_off<OFFS>(p, i);
-      const u32x2 v = *reinterpret_cast<const u32x2_a4*>(f + 12 + 4 * ihl);
-      sw = v.x >> 16;
-      dw = v.y & 0xffffu;
-    }
-    const uint32_t sport = bswap16(sw), dport = bswap16(dw);  // tcp_in.c:230-231
-    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
-    ixgwalk::walk(t, fg, bucket, tflags, src, dst, sport | (dport << 16), id, kind);
+DEV void prep_item(const DParams& p, uint32_t i, int lane, const Item& it, Pend& q) {
+  const bool valid = i < p.n;
+  const bool tcp = valid && ((it.rec.x >> 16) & 0xffu) == IXG_V_TCP;
+  const uint32_t ng = p.nfg + p.n_out, nlines = ng * IXG_PCB_BUCKETS;
+  const uint32_t fg = ixg_demux_group(it.rec.x & 0xffffu, p.fg_base, p.nfg, p.n_out);  // fgs[pkt->fg_id]
+  const uint32_t bucket = it.rec.w & (IXG_PCB_BUCKETS - 1u);                          // tcp_to_idx (tcp_in.c:233)
+  const uint32_t tflags = (it.rec.w >> 16) & 0xffu;
+  const uint32_t ihl = (it.h0.x >> 16) & 15u;  // frame byte 14
+  // src = bytes 26..29, dst = bytes 30..33 (raw, network order as loaded LE)
+  q.src = (it.h0.w >> 16) | (it.h1.x << 16);
+  q.dst = (it.h1.x >> 16) | (it.h1.y << 16);
+  uint32_t sw = it.h1.y >> 16, dw = it.h1.z & 0xffffu;  // ports: L4 bytes 0..3 at 14 + 4*ihl
+  if (tcp && ihl != 5u) {  // IP options: one more (dependent) load, rare
+    const uint8_t* f = p.base + frame_off<OFFS>(p, i);
+    const u32x2 v = *reinterpret_cast<const u32x2_a4*>(f + 12 + 4 * ihl);
+    sw = v.x >> 16;
+    dw = v.y & 0xffffu;
   }
-  const u32x2 o = {id, kind};
-  reinterpret_cast<u32x2*>(p.out)[i] = o;
+  q.ports = bswap16(sw) | (bswap16(dw) << 16);  // tcp_in.c:230-231
+  const bool look = tcp && fg < ng;
+  q.key = ixgwalk::lookup_key(valid ? (tcp ? (look ? fg : ixgwalk::kGrpNone) : ixgwalk::kGrpNotTcp) : ixgwalk::kGrpNoFrame,
+                              bucket, tflags);
+  ixgwalk::lines_issue(p.bline, nlines, look ? fg * IXG_PCB_BUCKETS + bucket : nlines, lane, q.piece);
+}
+
+DEV ixgwalk::Tables tables(const DParams& p) {
+  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
+}
+
+// match chunk c's pending lookups (buf: the wave's 4 KiB of LDS); the ones
+// the line cannot decide join the wave's queue sq
+DEV void finish_chunk(const DParams& p, uint32_t c, const Pend& q, int lane,
+                      __attribute__((address_space(3))) uint32_t* buf, ixgwalk::SlowQ& sq) {
+  u32x4 ln[4];
+  ixgwalk::lines_exchange(q.piece, lane, buf, ln);
+  const uint32_t i = c * 64u + (uint32_t)lane;
+  if ((q.key & 0x3fffu) == ixgwalk::kGrpNotTcp) reinterpret_cast<u32x2*>(p.out)[i] = u32x2{0u, (uint32_t)IXG_D_NONE};
+  ixgwalk::walk_line(tables(p), sq, i, q.key, q.src, q.dst, q.ports, ln[0], ln[1], ln[2], ln[3], lane, buf,
+                     reinterpret_cast<uint32_t*>(p.out), ixgwalk::Frames{nullptr, 0u});
 }
 
 template <bool OFFS>
 DEV void demux_loop(const DParams& p) {
+  __shared__ uint32_t sh_buf[kWaves][1024];
   const int lane = threadIdx.x & 63;
+  __attribute__((address_space(3))) uint32_t* buf =
+      (__attribute__((address_space(3))) uint32_t*)sh_buf[threadIdx.x >> 6];
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  uint32_t c = blockIdx.x * kWaves + (threadIdx.x >> 6);
+  uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
   if (c >= nchunks) return;
   Item cur;
   load_item<OFFS>(p, c, lane, cur);
+  Pend q;
+  uint32_t cq = kNoChunk;  // the chunk whose lookups q holds
+  ixgwalk::SlowQ sq;
+  sq.n = 0;
   for (;;) {
     const uint32_t cn = c + nw;
     Item nxt;
     load_item<OFFS>(p, cn < nchunks ? cn : c, lane, nxt);
-    const uint32_t i = c * 64u + (uint32_t)lane;
-    if (i < p.n) walk_item<OFFS>(p, i, cur);
+    if (cq != kNoChunk) finish_chunk(p, cq, q, lane, buf, sq);
+    prep_item<OFFS>(p, c * 64u + (uint32_t)lane, lane, cur, q);
+    cq = c;
     c = cn;
     if (c >= nchunks) break;
     cur = nxt;
   }
+  finish_chunk(p, cq, q, lane, buf, sq);
+  ixgwalk::slowq_flush(tables(p), sq, lane, reinterpret_cast<uint32_t*>(p.out), ixgwalk::Frames{nullptr, 0u});
 }
 
 }  // namespace

@@ -1534,20 +1534,15 @@ DEV void fastc_issue(const KParams& p, uint32_t cc, uint32_t nchunks, uint64_t l
 // the next iteration, after that chunk's frame loads are issued. (Matched at
 // once, the wait for the line -- vmcnt is in order -- also waited for the
 // next chunk's frames, loaded just before: the prefetch became synchronous.)
-// The 64 lines of a chunk are loaded by 4 lanes each (16 lines of 64 B per
-// wave instruction, 4 instructions): a lane loading its own line made every
-// instruction touch 64 lines, 4 times over, and the L1's per-line work, not
-// the bytes, bounded the kernel. The pieces are exchanged through the wave's
-// LDS buffer when the lookups are matched.
+// The lines come 4 lanes per line (ixgwalk::lines_issue) and reach their
+// lanes through the wave's LDS buffer when the lookups are matched.
 struct PendDmx {
-  u32x4 piece[4];  // piece k: bytes 16*(lane&3).. of the line of lane (lane>>2) + 16k
+  u32x4 piece[4];  // ixgwalk::lines_issue's pieces
   uint32_t c;      // the chunk (wave-uniform); kNoDmx: nothing pending
-  uint32_t fgt;    // group | TCP flags << 24; group kNotTcp / kNoFrame below
+  uint32_t key;    // ixgwalk::lookup_key
   uint32_t src, dst, ports;
 };
 constexpr uint32_t kNoDmx = 0xffffffffu;
-constexpr uint32_t kNotTcp = 0xffffffu;   // a valid frame that is not IXG_V_TCP
-constexpr uint32_t kNoFrame = 0xfffffeu;  // past the batch, or a deferred chunk
 
 DEV ixgwalk::Tables dmx_tables(const KParams& p) {
   return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
@@ -1559,52 +1554,33 @@ DEV void dmx_issue(const KParams& p, bool valid, uint32_t c, const Rec& r, uint3
                    int lane, PendDmx& q) {
   const bool tcp = valid && ((r.w0 >> 16) & 0xffu) == IXG_V_TCP;
   const uint32_t ng = p.nfg + p.n_out;
-  const uint32_t fg = tcp ? ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out) : kNoDmx;
+  const uint32_t fg = ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out);
   const bool look = tcp && fg < ng;
+  const uint32_t bucket = r.w3 & (IXG_PCB_BUCKETS - 1u);
   q.c = c;
-  q.fgt = (valid ? (tcp ? (look ? fg : kNotTcp - 2u) : kNotTcp) : kNoFrame) | (((r.w3 >> 16) & 0xffu) << 24);
+  q.key = ixgwalk::lookup_key(valid ? (tcp ? (look ? fg : ixgwalk::kGrpNone) : ixgwalk::kGrpNotTcp) : ixgwalk::kGrpNoFrame,
+                              bucket, (r.w3 >> 16) & 0xffu);
   q.src = src;
   q.dst = dst;
   q.ports = ports;
-  // the line's index in the snapshot (past the end: no line, the loads of
-  // its pieces read 0 without touching memory)
-  const uint32_t line = look ? fg * IXG_PCB_BUCKETS + (r.w3 & 0xffffu) : ng * IXG_PCB_BUCKETS;
-  const __amdgpu_buffer_rsrc_t rs = rsrc(p.bline, ng * IXG_PCB_BUCKETS * 64u);
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const uint32_t li = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * ((lane >> 2) + 16 * k), (int)line);
-    q.piece[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, li * 64u + 16u * (uint32_t)(lane & 3), 0, 0);
-  }
+  const uint32_t nlines = ng * IXG_PCB_BUCKETS;
+  ixgwalk::lines_issue(p.bline, nlines, look ? fg * IXG_PCB_BUCKETS + bucket : nlines, lane, q.piece);
 }
 
-// match the pending lookups (buf: the wave's 4 KiB of LDS, free)
-DEV void dmx_finish(const KParams& p, const PendDmx& q, int lane, lds_u32* buf) {
+// the queue reads the tuples back from the frames (fixed stride, ihl 5)
+DEV ixgwalk::Frames dmx_frames(const KParams& p) { return ixgwalk::Frames{p.base, p.stride}; }
+
+// match the pending lookups (buf: the wave's 4 KiB of LDS, free); the
+// ones the line cannot decide join the wave's queue sq
+DEV void dmx_finish(const KParams& p, const PendDmx& q, int lane, lds_u32* buf, ixgwalk::SlowQ& sq) {
   if (q.c == kNoDmx) return;
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    lds_u32* w = buf + 4 * (lane + 64 * k);  // = line (lane>>2)+16k, piece lane&3
-    w[0] = q.piece[k].x; w[1] = q.piece[k].y; w[2] = q.piece[k].z; w[3] = q.piece[k].w;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   u32x4 ln[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const lds_u32* r = buf + 16 * lane + 4 * k;
-    ln[k] = u32x4{r[0], r[1], r[2], r[3]};
-  }
-  // (the caller's next LDS writes must not pass these reads)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t g = q.fgt & 0xffffffu;
-  if (g == kNoFrame) return;
-  uint32_t id = 0, kind = IXG_D_NONE;
-  if (g != kNotTcp)
-    ixgwalk::walk_finish(dmx_tables(p), g, q.fgt >> 24, q.src, q.dst, q.ports, ln[0], ln[1], ln[2], ln[3], id, kind);
+  ixgwalk::lines_exchange(q.piece, lane, buf, ln);
+  const uint32_t i = q.c * 64u + (uint32_t)lane;
   typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-  reinterpret_cast<u32x2v*>(p.dmx)[q.c * 64u + (uint32_t)lane] = u32x2v{id, kind};
+  if ((q.key & 0x3fffu) == ixgwalk::kGrpNotTcp) reinterpret_cast<u32x2v*>(p.dmx)[i] = u32x2v{0u, (uint32_t)IXG_D_NONE};
+  ixgwalk::walk_line(dmx_tables(p), sq, i, q.key, q.src, q.dst, q.ports, ln[0], ln[1], ln[2], ln[3], lane, buf,
+                     reinterpret_cast<uint32_t*>(p.dmx), dmx_frames(p));
 }
 
 // A chunk the coalesced kernel could not take as fixed-shape, finished by
@@ -1657,14 +1633,18 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
   u32x4 cur[4];
   uint32_t Lc, seen = 0;
   PendDmx pend;
-  if (DMX) pend.c = kNoDmx;
+  ixgwalk::SlowQ sq;
+  if (DMX) {
+    pend.c = kNoDmx;
+    sq.n = 0;
+  }
   fastc_issue(p, c, nchunks, lim, lane, cur, Lc);
   for (;;) {
     const uint32_t cn = chunk_of(kth + 1);
     u32x4 nxt[4];
     uint32_t Ln;
     fastc_issue(p, cn, nchunks, lim, lane, nxt, Ln);
-    if (DMX) dmx_finish(p, pend, lane, buf);
+    if (DMX) dmx_finish(p, pend, lane, buf, sq);
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       lds_u32* w = buf + 4 * (lane + 64 * k);
@@ -1741,7 +1721,10 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     for (int k = 0; k < 4; k++) cur[k] = nxt[k];
     Lc = Ln;
   }
-  if (DMX) dmx_finish(p, pend, lane, buf);
+  if (DMX) {
+    dmx_finish(p, pend, lane, buf, sq);
+    ixgwalk::slowq_flush(dmx_tables(p), sq, lane, reinterpret_cast<uint32_t*>(p.dmx), dmx_frames(p));
+  }
   publish_classes(p, seen, lane);
   if (DRAIN) {
     // the wave's own deferred chunks (its first 64: a wave has ~8; the rest,

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--separate", action="store_true",
                     help="time the separate demux pass (ixg_demux_batch_dev) over RX records made once")
+    ap.add_argument("--plain", action="store_true", help="time the RX launch alone (no demux) on the same frames")
     args = ap.parse_args()
     import torch
     import bench
@@ -53,7 +54,9 @@ def main():
 
     def launch(v):
         r, d = outs[v]
-        if args.separate:
+        if args.plain:
+            wl.launch(engs[v], s.cuda_stream)
+        elif args.separate:
             demux.batch_dev(engs[v], wl.blob.data_ptr(), None, wl.stride, wl.n, r.data_ptr(), d.data_ptr(),
                             s.cuda_stream)
         else:
@@ -78,7 +81,8 @@ def main():
     res = {v: {"median_ms": round(float(np.median(t)), 4), "min_ms": round(float(np.min(t)), 4),
                "frac80": round(wl.n * 80 / (np.median(t) * 1e-3) / 8e12, 4), "same_as_first": same[v]}
            for v, t in times.items()}
-    print(json.dumps({"workload": ("separate" if args.separate else "fused") + " demux over C2", "results": res}),
+    kind = "plain RX (no demux)" if args.plain else ("separate" if args.separate else "fused") + " demux"
+    print(json.dumps({"workload": kind + " over C2", "results": res}),
           flush=True)
 
 

@@ -1,0 +1,11 @@
+#!/bin/bash
+set -e
+cd /root/repo
+export TMPDIR=/tmp
+O=gpurun_out/${OUTDIR:-r3l}; mkdir -p $O
+timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "demux or dmx or fdir" > $O/pytest.log 2>&1
+timeout -k 10 200 python3 -u tools/ab_demux.py --libs ix_amd/libixgrx.so,tools/ablib/coop.so,tools/ablib/head.so > $O/ab_demux.json 2>$O/ab.err
+timeout -k 10 200 python3 -u tools/ab_demux.py --separate --libs ix_amd/libixgrx.so,tools/ablib/coop.so > $O/ab_demux_sep.json 2>>$O/ab.err
+timeout -k 10 200 python3 -u tools/ab_demux.py --plain --libs ix_amd/libixgrx.so,tools/ablib/coop.so > $O/ab_plain.json 2>>$O/ab.err
+tools/dmx_counters.sh ${OUTDIR:-r3l}/pmc > $O/pmc_report.txt 2>&1
+echo ok
