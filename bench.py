@@ -291,6 +291,12 @@ def parity_leg(checks, key) -> dict:
             ok = ev0 is not None and len(ev0) == len(eev) and \
                 np.array_equal(ev0.view(np.uint8), eev.view(np.uint8)) and np.array_equal(f0, eidx.astype(np.int64))
             res["events"] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
+        elif c[0] == "tcpx":
+            _, pool, rec, ext0, tiled = c
+            er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
+            eext, _ = oracle.tcp_ext_batch(pool.blob, pool.off, pool.stride, er)
+            ok = np.array_equal(rec, er) and np.array_equal(ext0, eext)
+            res["tcpx"] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
         elif c[0] == "tx":
             _, kind, (buf, segs, smac, dmacs, out, out_len), tiled = c
             size = int(segs["out_off"][-1]) + 2048
@@ -526,6 +532,48 @@ def events_line(dev, key, steps: int, rank: int, eng_for):
             "mevents_per_s": round(m * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
             "alg_bytes_per_frame": round(alg / n, 1), "roofline_frac": round(alg / k / 1e9 / PEAK_HBM_GBPS, 4),
             "parity": "tiled-consistent" if check[-1] else "MISMATCH"}, check
+
+
+def tcpx_line(dev, steps: int, rank: int, eng_for):
+    """The rest of the tcp_input head (tcp_in.c:230-241) over
+    C2's shape: 16M 64-B TCP frames tiled from 2^16 distinct ones; the RX
+    records come from one untimed RX launch, a step = one
+    ixg_tcp_ext_batch_dev launch (struct ixg_tcp_ext per frame)."""
+    import torch
+    from ix_amd import tcpx
+    wl = Workload("c2", seed=0x1BF100 + 97 * rank, dev=dev, pool=1 << 16)
+    eng = eng_for(0)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    wl.launch(eng, sp)
+    ext = torch.empty((wl.n, 16), dtype=torch.uint8, device=dev)
+
+    def launch():
+        tcpx.batch_dev(eng, wl.blob.data_ptr(), None, wl.stride, wl.out.data_ptr(), wl.n, ext.data_ptr(), 0, sp)
+    for _ in range(LINE_WARMUP):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, c in ev:
+        a.record(stream)
+        launch()
+        c.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = float(np.mean([a.elapsed_time(c) * 1e-3 for a, c in ev]))
+    v = ext.view(wl.reps, -1, 16)
+    tiled = bool(torch.equal(v, v[:1].expand(wl.reps, -1, -1)))
+    # algorithmic bytes per frame: the record (16), the IHL byte, the 14 header
+    # bytes the head converts (ports, seqno, ackno, wnd) and the 16-byte ext
+    # written; the frame lines they sit in are the frame itself at C2's size
+    alg = 16 + 1 + 14 + 16
+    check = ("tcpx", wl.pool, wl.out.view(wl.reps, -1, 16)[0].cpu().numpy(), v[0].cpu().numpy(), tiled)
+    return {"workload": "tcp_input head rest (seqno/ackno/wnd/tcplen) over C2: 16M x 64B TCP frames; kernel ixg_tcpx_s",
+            "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
+            "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4),
+            "gbps_frame_bytes": round((16 + wl.stride + 16) * wl.n / k / 1e9, 1),
+            "parity": "tiled-consistent" if tiled else "MISMATCH"}, check
 
 
 def tx_line(dev, steps: int, eng, kind: str, n: int):
@@ -1013,6 +1061,11 @@ def main():
         res["events"], echk = events_line(dev, key, max(5, args.steps // 2), rank, engine)
         checks.append(echk)
         torch.cuda.empty_cache()
+    if not args.no_demux and args.workload == "c2":
+        torch.cuda.empty_cache()
+        res["tcpx"], xchk = tcpx_line(dev, max(5, args.steps // 2), rank, engine)
+        checks.append(xchk)
+        torch.cuda.empty_cache()
     if not args.no_tx and args.workload == "c2":
         torch.cuda.empty_cache()
         res["tx"] = {}
@@ -1066,6 +1119,8 @@ def main():
             res["tx"][kind]["parity"] = par["tx_" + kind]
         if "events" in res:
             res["events"]["parity"] = par["events"]
+        if "tcpx" in res:
+            res["tcpx"]["parity"] = par["tcpx"]
         if "bad_csum" in res:
             res["bad_csum"]["parity"] = par["c2b"]
     if rank == 0:

@@ -22,10 +22,11 @@
  * (a hipStream_t), device buffers as plain pointers.
  *
  * Threading follows IX's per-CPU model: one context per host thread; calls on
- * one context are not thread-safe. The library never frees or modifies an
- * input frame (the reference rewrites TCP header fields to host order in
- * place, tcp_in.c:230-238, and UDP writes an ip_tuple over the frame start,
- * udp.c:81-86; both are host-side consumers' business here).
+ * one context are not thread-safe. The library never frees an input frame
+ * and modifies one only when asked to: the reference rewrites TCP header
+ * fields to host order in place (tcp_in.c:230-238; IXG_TCPX_INPLACE of
+ * ixg_tcp_ext_batch_dev) and UDP writes an ip_tuple over the frame start
+ * (udp.c:81-86; IXG_EV_UDP_TUPLE of ixg_ev_batch_dev).
  */
 #ifndef IXGRX_H
 #define IXGRX_H
@@ -316,6 +317,36 @@ struct ixg_rx_ops {
  * (dp/core/ethqueue.c:117-149). */
 uint32_t ixg_rx_dispatch(void *const *mbufs, const struct ixg_rx_rec *recs, uint32_t n,
 			 const struct ixg_rx_ops *ops, void *user);
+
+/* ---- the rest of the tcp_input head: seqno/ackno/wnd/tcplen ------------- */
+
+/* What tcp_input computes for a segment after the doff strip and before the
+ * PCB lookup (dp/net/tcp_in.c:230-241): the header fields converted to host
+ * order, kept in its LWIP_Context, and tcplen. One per frame, in input order;
+ * all zero unless the record's verdict is IXG_V_TCP (or IXG_V_TCP6 under
+ * IXG_F_IPV6, the same conversions at L4 offset 54). */
+struct ixg_tcp_ext {
+	uint32_t seqno;    /* ntohl(tcphdr->seqno) (tcp_in.c:236) */
+	uint32_t ackno;    /* ntohl(tcphdr->ackno) (:237) */
+	uint16_t wnd;      /* ntohs(tcphdr->wnd) (:238) */
+	uint16_t tcplen;   /* p->tot_len after the strip + 1 if FIN or SYN (:241), u16 as lwIP keeps it */
+	uint16_t src_port; /* ntohs(tcphdr->src): the remote port (:230) */
+	uint16_t dst_port; /* ntohs(tcphdr->dest): the local port (:231) */
+};
+
+/* flags of ixg_tcp_ext_batch_dev */
+#define IXG_TCPX_INPLACE (1u << 0) /* also rewrite each such segment's header as
+                                      tcp_input leaves it: src, dest, seqno,
+                                      ackno and wnd in host order, in place
+                                      (tcp_in.c:230-238), so the unmodified
+                                      rest of tcp_input (tcp_process,
+                                      tcp_receive) can read the frame */
+
+/* Device-resident: frames (as for ixg_rx_batch_dev; with IXG_TCPX_INPLACE
+ * writable) and the records ixg_rx_batch_dev produced for them; one
+ * ixg_tcp_ext per frame into d_ext. Asynchronous on `stream`. 0 or -errno. */
+int ixg_tcp_ext_batch_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec,
+			  uint32_t n, struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream);
 
 /* ---- PCB demux: the tcp_input step after the head ---- */
 

@@ -11,6 +11,7 @@
 
 #include "ixgrx_ctx.h"
 #include "ixgrx_demux.h"
+#include "ixgrx_tcpx.h"
 #include "ixgrx_tx.h"
 #include "ixgrx_ev.h"
 
@@ -917,6 +918,32 @@ int ixg_rx_demux_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t 
 		return -EIO;
 	return ixg_launch_ds(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, d_dmx,
 			     0, (hipStream_t)stream);
+}
+
+/* ---- the rest of the tcp_input head (tcp_in.c:230-241) ---------------------- */
+
+int ixg_tcp_ext_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec, uint32_t n,
+			  struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || (n && (!fr->base || !d_rec || !d_ext)) || (flags & ~IXG_TCPX_INPLACE))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)fr->base & 3) || (!fr->off && (fr->stride & 3)) || ((uintptr_t)d_rec & 15) ||
+	    ((uintptr_t)d_ext & 15) || ((uintptr_t)fr->off & 7))
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	struct ixg_xparams p;
+	memset(&p, 0, sizeof(p));
+	p.base = (uint8_t *)(uintptr_t)fr->base;
+	p.off = fr->off;
+	p.rec = d_rec;
+	p.ext = d_ext;
+	p.stride = fr->stride;
+	p.n = n;
+	p.flags = flags;
+	return ixgrx_tcpx_launch(&p, stream) == 0 ? 0 : -EIO;
 }
 
 int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, const uint16_t *len, uint32_t stride,

@@ -740,6 +740,41 @@ int ixgo_demux_batch(const struct ixg_demux_tables *t, uint32_t fg_base, const u
 
 /* ---- TX: header build + checksums ------------------------ */
 
+/* ---- the rest of the tcp_input head (tcp_in.c:230-241) --------------------- */
+
+int ixgo_tcp_ext_batch(uint8_t *base, const uint64_t *off, uint32_t stride, const struct ixg_rx_rec *rec,
+		       uint32_t n, uint32_t flags, struct ixg_tcp_ext *ext)
+{
+	for (uint32_t i = 0; i < n; i++) {
+		struct ixg_tcp_ext *e = &ext[i];
+		memset(e, 0, sizeof(*e));
+		const uint8_t v = rec[i].verdict;
+		if (v != IXG_V_TCP && v != IXG_V_TCP6)
+			continue;
+		uint8_t *f = base + (off ? off[i] : (uint64_t)i * stride);
+		/* p->payload = the TCP header: after ip_input's ihl*4 (ip.c:95-98,
+		 * tcp_input_tmp misc.c:61-62), or the extension's fixed 40 */
+		uint8_t *t = f + (v == IXG_V_TCP ? 14u + 4u * (f[14] & 15u) : 54u);
+		e->src_port = bswap16(ld16(t));     /* :230 */
+		e->dst_port = bswap16(ld16(t + 2)); /* :231 */
+		e->seqno = __builtin_bswap32(ld32(t + 4)); /* :236 */
+		e->ackno = __builtin_bswap32(ld32(t + 8)); /* :237 */
+		e->wnd = bswap16(ld16(t + 14));     /* :238 */
+		/* :240-241: p->tot_len after the doff strip is the record's l4_len;
+		 * TCP_FIN | TCP_SYN = 0x03 */
+		e->tcplen = (uint16_t)(rec[i].l4_len + ((rec[i].tcp_flags & 0x03u) ? 1u : 0u));
+		if (flags & IXG_TCPX_INPLACE) {
+			/* the same fields written back in host order (:230-238) */
+			memcpy(t, &e->src_port, 2);
+			memcpy(t + 2, &e->dst_port, 2);
+			memcpy(t + 4, &e->seqno, 4);
+			memcpy(t + 8, &e->ackno, 4);
+			memcpy(t + 14, &e->wnd, 2);
+		}
+	}
+	return 0;
+}
+
 /*
  * in_pseudo + inet_chksum_pseudo (dp/lwip/inet_chksum.c:324-357): the seed
  * lwIP leaves in the TCP checksum field for the NIC:

@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
         L.ixgo_tx_batch.restype = i32
         L.ixgo_ev_batch.argtypes = [vp, vp, u32, vp, vp, vp, u32, u32, ctypes.c_uint64, u32, vp, vp]
         L.ixgo_ev_batch.restype = u32
+        L.ixgo_tcp_ext_batch.argtypes = [vp, vp, u32, vp, u32, u32, vp]
+        L.ixgo_tcp_ext_batch.restype = i32
         _lib = L
     return _lib
 
@@ -253,3 +255,22 @@ def ev_batch(blob: np.ndarray, off, stride: int, rec: np.ndarray, dmx, pcbs, iom
                         None if d is None else d.ctypes.data, pc.ctypes.data if pc.size else None, pc.size, n,
                         iomap_base, flags, ev.ctypes.data, fi.ctypes.data)
     return ev[:k].copy(), fi[:k].copy(), b
+
+
+TCPX_DTYPE = np.dtype([("seqno", "<u4"), ("ackno", "<u4"), ("wnd", "<u2"), ("tcplen", "<u2"),
+                       ("src_port", "<u2"), ("dst_port", "<u2")])
+
+
+def tcp_ext_batch(blob: np.ndarray, off, stride: int, rec: np.ndarray, flags: int = 0):
+    """The rest of the tcp_input head (oracle/ixgrx_oracle.c
+    ixgo_tcp_ext_batch). Returns (struct ixg_tcp_ext rows as (n, 16) u8, the
+    frames after the optional in-place conversion)."""
+    L = lib()
+    b = np.ascontiguousarray(blob, dtype=np.uint8).copy()
+    n = int(rec.shape[0])
+    offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    r = np.ascontiguousarray(rec).view(np.uint8).reshape(n, 16)
+    ext = np.zeros((max(n, 1), 16), dtype=np.uint8)
+    L.ixgo_tcp_ext_batch(b.ctypes.data, None if offa is None else offa.ctypes.data, stride, r.ctypes.data, n, flags,
+                         ext.ctypes.data)
+    return ext[:n].copy(), b

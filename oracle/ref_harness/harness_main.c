@@ -31,7 +31,11 @@
  *                   struct ixg_fdir_filter[nf].
  * Output file (LE): "IXGRXOUT", u32 n, struct ixg_rx_rec[n] (16 B), u32 csum[n],
  *                   u8 confirm[n] (0: eth_input did not drop the frame; 1: it
- *                   did and confirm_drop pinned the reason; 2: not pinned).
+ *                   did and confirm_drop pinned the reason; 2: not pinned),
+ *                   "TCPX", struct ixg_tcp_ext[n], u8 hdr[n][16] (the rest of
+ *                   the tcp_input head from the reference's own tcp_input,
+ *                   ref_tcphead.c: its LWIP_Context fields and the segment's
+ *                   first 16 bytes as it converted them in place).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -197,6 +201,51 @@ static const struct ixg_fdir_filter *fdir;
 static uint32_t n_fdir;
 static unsigned int fdir_cpu;
 
+/* the rest of the tcp_input head (tcp_in.c:230-241) for the frame one() just
+ * classified: ixg_tcp_ext and the segment's first 16 bytes as the head leaves
+ * them (converted to host order in place); zero for every other verdict */
+static struct ixg_tcp_ext th_ext;
+static uint8_t th_hdr[16];
+
+static uint16_t h16(const uint8_t *p)
+{
+	uint16_t v;
+	memcpy(&v, p, 2);
+	return v;
+}
+static uint32_t h32(const uint8_t *p)
+{
+	uint32_t v;
+	memcpy(&v, p, 4);
+	return v;
+}
+
+/* fill th_ext from a header already in host order and the post-strip length */
+static void ext_from(const uint8_t *hdr, uint16_t tot_len, uint8_t tcp_flags)
+{
+	th_ext.seqno = h32(hdr + 4);
+	th_ext.ackno = h32(hdr + 8);
+	th_ext.wnd = h16(hdr + 14);
+	/* tcp_in.c:241: TCP_FIN 0x01, TCP_SYN 0x02 */
+	th_ext.tcplen = (uint16_t)(tot_len + ((tcp_flags & 0x03) ? 1 : 0));
+	th_ext.src_port = h16(hdr);
+	th_ext.dst_port = h16(hdr + 2);
+}
+
+/* [V6] the extension's TCP: the reference never parses IPv6; the head's
+ * conversions restated over the segment at 54 */
+static void ext_v6(const uint8_t *f, uint16_t tot_len, uint8_t tcp_flags)
+{
+	const uint8_t *t = f + 54;
+	th_hdr[0] = t[1], th_hdr[1] = t[0], th_hdr[2] = t[3], th_hdr[3] = t[2];
+	for (int k = 0; k < 4; k++) {
+		th_hdr[4 + k] = t[7 - k];
+		th_hdr[8 + k] = t[11 - k];
+	}
+	th_hdr[12] = t[12], th_hdr[13] = t[13], th_hdr[14] = t[15], th_hdr[15] = t[14];
+	ext_from(th_hdr, tot_len, tcp_flags);
+}
+
 static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, uint8_t *mbuf,
 		struct ixg_rx_rec *r, uint32_t *csum, uint8_t *confirm, uint32_t idx)
 {
@@ -206,6 +255,8 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 	uint8_t flags = 0;
 
 	memset(r, 0, sizeof(*r));
+	memset(&th_ext, 0, sizeof(th_ext));
+	memset(th_hdr, 0, sizeof(th_hdr));
 	*confirm = 0;
 	r->pcb_bucket = IXG_NO_BUCKET;
 	memset(f, 0, sizeof(f));
@@ -304,6 +355,7 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 			r->l4_off = (uint16_t)(54 + doff * 4);
 			r->l4_len = nl;
 			r->tcp_flags = f[54 + 13] & 0x3f;
+			ext_v6(f, nl, r->tcp_flags);
 		} else {
 			uint16_t ulen = B16z(f, L, 54 + 4);
 			if (54 + ulen > L) { drop(r, IXG_V_DROP_UDP_LEN); return; }
@@ -337,11 +389,37 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 		uint16_t n = ref_cap.l4_len;
 		if (off != l4)
 			die("tcp l4 offset mismatch", idx);
-		/* [TCP] tcp_input head (tcp_in.c:189,221-222) */
-		if (n < 20) { drop(r, IXG_V_DROP_TCP_SHORT); return; }
+		/* the reference's own tcp_input over the segment tcp_input_tmp
+		 * hands it (ref_tcphead.c): passed or dropped, and what the head
+		 * converted in place */
+		uint16_t tot_after = 0;
+		const int passed = ref_tcp_head(f + off, n, raw32(f + 26), raw32(f + 30), th_hdr, &tot_after);
+		/* [TCP] tcp_input head (tcp_in.c:189,221-222), which the real head must agree with */
+		if (n < 20) {
+			if (passed) die("tcp_input passed a segment shorter than 20", idx);
+			memset(th_hdr, 0, sizeof(th_hdr));
+			drop(r, IXG_V_DROP_TCP_SHORT);
+			return;
+		}
 		uint8_t doff = f[off + 12] >> 4; /* TCPH_HDRLEN */
 		uint16_t nl;
-		if (ref_pbuf_header_rom(n, (int16_t)-(doff * 4), &nl)) { drop(r, IXG_V_DROP_TCP_HDRLEN); return; }
+		if (ref_pbuf_header_rom(n, (int16_t)-(doff * 4), &nl)) {
+			if (passed) die("tcp_input passed a segment with doff*4 > l4len", idx);
+			memset(th_hdr, 0, sizeof(th_hdr));
+			drop(r, IXG_V_DROP_TCP_HDRLEN);
+			return;
+		}
+		if (!passed || tot_after != nl)
+			die("tcp_input head disagrees with the pbuf_header restatement", idx);
+		ext_from(th_hdr, tot_after, f[off + 13] & 0x3f);
+		/* no PCB: tcp_rst(ackno, seqno + tcplen, ..., dest, src) unless RST (tcp_in.c:503-506) */
+		if (f[off + 13] & 0x04) {
+			if (ref_th.rst_called) die("tcp_rst for a segment carrying RST", idx);
+		} else if (ref_th.rst_called != 1 || ref_th.rst_seqno != th_ext.ackno ||
+			   ref_th.rst_ackno != th_ext.seqno + th_ext.tcplen || ref_th.rst_local_port != th_ext.dst_port ||
+			   ref_th.rst_remote_port != th_ext.src_port) {
+			die("tcp_rst arguments disagree with the converted header", idx);
+		}
 		r->verdict = IXG_V_TCP;
 		r->l4_off = (uint16_t)(off + doff * 4);
 		r->l4_len = nl;
@@ -433,10 +511,14 @@ int main(int argc, char **argv)
 	struct ixg_rx_rec *recs = calloc(n + 1, sizeof(*recs));
 	uint32_t *cs = calloc(n + 1, sizeof(*cs));
 	uint8_t *cf = calloc(n + 1, 1);
+	struct ixg_tcp_ext *ext = calloc(n + 1, sizeof(*ext));
+	uint8_t *hdr = calloc(n + 1, 16);
 	for (uint32_t i = 0; i < n; i++) {
 		if (len[i] > IXG_MBUF_DATA_LEN || (uint64_t)off[i] + len[i] > blob_len)
 			die("frame does not fit an mbuf", i);
 		one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], &cf[i], i);
+		ext[i] = th_ext;
+		memcpy(hdr + 16 * (size_t)i, th_hdr, 16);
 	}
 	FILE *fo = fopen(argv[2], "wb");
 	if (!fo)
@@ -446,6 +528,9 @@ int main(int argc, char **argv)
 	fwrite(recs, sizeof(*recs), n, fo);
 	fwrite(cs, 4, n, fo);
 	fwrite(cf, 1, n, fo);
+	fwrite("TCPX", 1, 4, fo);
+	fwrite(ext, sizeof(*ext), n, fo);
+	fwrite(hdr, 16, n, fo);
 	fclose(fo);
 	if (tsec > 0 && n > 0) {
 		struct timespec t0, t1;

@@ -52,4 +52,17 @@ void ref_ev_set_iomap(uint64_t iomap_offset);
 uint64_t ref_iomap(const void *p);
 void ref_ev_udp(void *addr, size_t len, void *id, uint64_t out[5]);
 void ref_ev_tcp(uint64_t handle, unsigned long cookie, void *addr, size_t len, uint64_t out[5]);
+
+/* the tcp_input head run for real (ref_tcphead.c): what tcp_rst received */
+struct ref_tcphead_cap {
+	int rst_called;
+	uint32_t rst_seqno, rst_ackno; /* tcp_rst(ackno, seqno + tcplen, ...) (tcp_in.c:505) */
+	uint16_t rst_local_port, rst_remote_port;
+};
+extern struct ref_tcphead_cap ref_th;
+/* runs tcp_input over one segment with empty PCB lists; returns 1 when the
+ * segment passed the head. hdr_out: the segment's first 16 bytes afterwards
+ * (converted in place); tot_len_after: the pbuf length after the strip */
+int ref_tcp_head(const uint8_t *seg, uint16_t seg_len, uint32_t src_raw, uint32_t dst_raw, uint8_t hdr_out[16],
+		 uint16_t *tot_len_after);
 #endif

@@ -44,7 +44,9 @@ def fdir_filter(f: bytes, swap: bool = False) -> bytes:
 
 
 def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir: list[bytes] | None = None,
-            cpu: int = 0):
+            cpu: int = 0, full: bool = False):
+    """(records, residuals) from the reference's eth_input; full: also the
+    rest of the tcp_input head from its tcp_input (tcpx, tcpx_hdr)."""
     lens = np.array([len(f) for f in frames], dtype=np.uint16)
     offs = np.zeros(len(frames), dtype=np.uint32)
     if frames:
@@ -80,7 +82,14 @@ def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir
     eth_input_reasons = ((verdict >= 0x80) & (verdict <= 0x87)) | ((verdict >= 0x8b) & (verdict <= 0x8d))
     assert not (confirm == 2).any(), f"drop reasons not confirmed by the reference: {np.nonzero(confirm == 2)[0][:20]}"
     assert ((confirm == 1) == eth_input_reasons).all(), "a drop reason without a reference confirmation"
-    return rec, csum
+    # the rest of the tcp_input head from the reference's own tcp_input
+    # (ref_tcphead.c): struct ixg_tcp_ext per frame and the segment's first 16
+    # bytes as tcp_input converted them in place
+    o = 12 + 21 * n
+    assert raw[o:o + 4] == b"TCPX"
+    tcpx = np.frombuffer(raw, dtype=np.uint8, count=16 * n, offset=o + 4).reshape(n, 16).copy()
+    tcpx_hdr = np.frombuffer(raw, dtype=np.uint8, count=16 * n, offset=o + 4 + 16 * n).reshape(n, 16).copy()
+    return (rec, csum, tcpx, tcpx_hdr) if full else (rec, csum)
 
 
 # ---------------------------------------------------------------- frames
@@ -309,7 +318,7 @@ def fuzz_frames(rng: np.random.Generator, n: int) -> list[bytes]:
 
 def save(name: str, frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, note: str,
          fdir: list[bytes] | None = None, cpu: int = 0):
-    rec, csum = run_ref(frames, key, nb, dev, flags, fdir, cpu)
+    rec, csum, tcpx, tcpx_hdr = run_ref(frames, key, nb, dev, flags, fdir, cpu, full=True)
     tr = traces.pack(frames)
     path = os.path.join(HERE, name + ".npz")
     extra = {}
@@ -319,7 +328,7 @@ def save(name: str, frames: list[bytes], key: bytes, nb: int, dev: int, flags: i
     np.savez_compressed(path, blob=tr.blob, off=tr.off, len=tr.len,
                         key=np.frombuffer(key, np.uint8), nb_rx_fgs=np.uint16(nb),
                         dev_idx=np.uint16(dev), flags=np.uint32(flags), rec=rec, csum=csum,
-                        note=np.array(note), **extra)
+                        tcpx=tcpx, tcpx_hdr=tcpx_hdr, note=np.array(note), **extra)
     v = rec[:, 2]
     print(f"{name}: {len(frames)} frames, verdicts {dict(zip(*np.unique(v, return_counts=True)))}")
 
