@@ -282,7 +282,12 @@ constexpr int kShapeFixed = 0, kShapeV4 = 1, kShapeV6 = 2, kShapeAny = 3;
 // at run time: a graph captured before the filters changed sees the new set.
 // Returns the outbound flow group of a matching frame, or 0xffffffff.
 DEV uint32_t fdir_match(const KParams& p, uint32_t src, uint32_t dst, uint32_t ports) {
-  const u32x4 hdr = *reinterpret_cast<const u32x4*>(p.fdir);  // {mask, fg, 0, 0}: scalar
+  // {mask, fg, 0, 0}: a scalar load through the constant address space (the
+  // host writes the table only between launches). Read as a plain global
+  // load it was a vector load, and its s_waitcnt vmcnt(0) also waited for
+  // every frame load the wave had in flight (the next chunk's prefetch)
+  typedef const __attribute__((address_space(4))) u32x4 cu32x4;
+  const u32x4 hdr = *(cu32x4*)(p.fdir);
   if (hdr.x == 0u) return 0xffffffffu;
   const u32x4* slot = reinterpret_cast<const u32x4*>(p.fdir) + 1;
   uint32_t k = ixg_fdir_hash(src, dst, ports) & hdr.x;
@@ -1668,10 +1673,13 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
 #pragma unroll
       for (int j = 3; j < 16; j++) d[j] &= ones((int)Lc - 4 * j < 0 ? 0 : (int)Lc - 4 * j);
     }
-    const uint32_t etype = (byte_at(d, 12) << 8) | byte_at(d, 13);
-    const uint32_t ip_len = (byte_at(d, 16) << 8) | byte_at(d, 17);
-    const bool fast = !valid || (Lc <= 64u && etype == 0x0800u && byte_at(d, 14) == 0x45u && ip_len >= 20 &&
-                                 14 + ip_len <= 64 && (lane != 63 || Lc <= p.stride || p.overlap));
+    // fixed-shape: ethertype 0x0800 and version/ihl 0x45 (bytes 12..14 as
+    // one masked dword), 20 <= ip_len <= 50 (14 + ip_len <= 64), L <= 64.
+    // Non-short-circuit `&` / `|`: evaluated straight through, with no
+    // exec-mask branches (a `&&` chain here compiled to nested branches)
+    const uint32_t ip_len = bswap16(d[4] & 0xffffu);  // bytes 16..17
+    const bool fast = !valid | ((Lc <= 64u) & ((d[3] & 0x00ffffffu) == 0x00450008u) & (ip_len - 20u <= 30u) &
+                                ((lane != 63) | (Lc <= p.stride) | (p.overlap != 0u)));
     const bool all_fast = wave_all(fast);
     // chunks that are not fixed-shape are finished after the loop (DRAIN)
     // or flagged for the general kernels
@@ -1685,8 +1693,8 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     // the lean path (lean_tcp) when every frame is a TCP segment tcp_input
     // accepts and all share one IP total length
     const uint32_t ipl = __builtin_amdgcn_readfirstlane(ip_len);
-    const bool tcpok = (d[5] & 0xff00ff3fu) == 0x06000000u && 14u + ipl <= Lc && ((d[11] >> 18) & 0x3cu) <= ipl - 20u;
-    const bool lean = all_fast && ipl >= 40u && wave_all(!valid || (ip_len == ipl && tcpok));
+    const bool tcpok = ((d[5] & 0xff00ff3fu) == 0x06000000u) & (14u + ipl <= Lc) & (((d[11] >> 18) & 0x3cu) <= ipl - 20u);
+    const bool lean = all_fast & (ipl >= 40u) & wave_all(!valid | ((ip_len == ipl) & tcpok));
     const uint32_t rem = p.n - c * 64u < 64u ? p.n - c * 64u : 64u;
     if (DMX) {
       // (a deferred chunk's records and demux records are the general kernel's)
