@@ -108,3 +108,26 @@ def test_p2p_pieces_cover_in_order():
     b = torch.arange(100, dtype=torch.uint8)
     assert [p.numel() for p in shard._pieces(b, 30)] == [30, 30, 30, 10]
     assert len(shard._pieces(torch.empty(0, dtype=torch.uint8), 30)) == 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_parity_vs_oracle():
+    """bench.py at N = 2 (two gloo ranks sharing the box's card, as the
+    driver's N > 1 runs but without RCCL): rank 0 prints one JSON line whose
+    every device line was checked against the oracle (parity_vs_oracle),
+    including the records gathered back from rank 1 (c4_strong)."""
+    import json
+    port = _free_port()
+    env = dict(os.environ, IXG_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(os.path.dirname(HERE), "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--n", str(1 << 16), "--secondary", "", "--extra", "c5r",
+           "--strong-n", str(1 << 16), "--no-copy", "--no-tx", "--no-demux", "--cpu-seconds", "0.5"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith("{")][-1]
+    d = json.loads(line)
+    assert d["n_gpus"] == 2
+    par = d["parity_vs_oracle"]
+    assert par["c2"] == "ok" and par["c2b"] == "ok" and par["c5r"] == "ok" and par["c4_strong"] == "ok", par
+    assert d["c4_strong"]["slice_frames"][0] + d["c4_strong"]["slice_frames"][1] >= 1 << 16
