@@ -908,7 +908,7 @@ def main():
     ap.add_argument("--xgmi", action="store_true", help="N > 1: add the equal-slice RCCL scatter/gather leg")
     ap.add_argument("--no-strong", action="store_true", help="skip the C4 one-batch strong-split line")
     ap.add_argument("--strong-n", type=int, default=C4_FRAMES, help="C4 strong-split batch size (frames)")
-    ap.add_argument("--n", type=int, default=None, help="override frames per GPU")
+    ap.add_argument("--frames", "--n", dest="n", type=int, default=None, help="override frames per GPU")
     args = ap.parse_args()
 
     import torch

@@ -121,7 +121,7 @@ def test_bench_two_ranks_parity_vs_oracle():
     env = dict(os.environ, IXG_BENCH_BACKEND="gloo")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(os.path.dirname(HERE), "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--n", str(1 << 16), "--secondary", "", "--extra", "c5r",
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--frames", str(1 << 16), "--secondary", "", "--extra", "c5r",
            "--strong-n", str(1 << 16), "--no-copy", "--no-tx", "--no-demux", "--cpu-seconds", "0.5"]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
