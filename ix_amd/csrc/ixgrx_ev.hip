@@ -138,12 +138,27 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_emit(EParams p) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
-  for (uint32_t k = 0, c = ev_chunk(0, nw, nchunks); c < nchunks; c = ev_chunk(++k, nw, nchunks)) {
+  // the chunk bases were written by the kernels before this one: scalar
+  // loads through the constant address space (counted on lgkmcnt, so they
+  // never wait for the records in flight)
+  typedef const __attribute__((address_space(4))) uint32_t cu32;
+  uint32_t k = 0, c = ev_chunk(0, nw, nchunks);
+  if (c >= nchunks) return;
+  Ev e = classify(p, c * 64u + (uint32_t)lane);
+  for (;;) {
+    // the next chunk's records and demux records are loaded before this
+    // chunk's descriptors are built (one chunk of software pipelining)
+    const uint32_t cn = ev_chunk(++k, nw, nchunks);
+    const Ev en = classify(p, cn * 64u + (uint32_t)lane);  // (i >= n past the end: nothing valid)
     const uint32_t i = c * 64u + (uint32_t)lane;
-    const Ev e = classify(p, i);
     const uint64_t m = __ballot(e.on);
-    if (m == 0) continue;
-    const uint32_t base = p.group_base[c >> 6] + p.chunk_base[c], r = rank_of(m);
+    if (m == 0) {
+      if (cn >= nchunks) break;
+      c = cn;
+      e = en;
+      continue;
+    }
+    const uint32_t base = *(cu32*)(p.group_base + (c >> 6)) + *(cu32*)(p.chunk_base + c), r = rank_of(m);
     if (e.on) {
       const uint64_t foff = p.off ? p.off[i] : (uint64_t)i * p.stride;
       const uint64_t fio = p.iomap_base + foff;  // iomap(frame start)
@@ -195,10 +210,13 @@ extern "C" __global__ void __launch_bounds__(kBlock) ixg_ev_emit(EParams p) {
     // by lane (5 per descriptor, at most 5 stores per lane)
     uint64_t* out = reinterpret_cast<uint64_t*>(p.ev + base);
     const uint32_t nq = 5u * (uint32_t)__popcll(m);
-    for (uint32_t k = (uint32_t)lane; k < nq; k += 64u) out[k] = buf[k];
+    for (uint32_t q = (uint32_t)lane; q < nq; q += 64u) out[q] = buf[q];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (cn >= nchunks) break;
+    c = cn;
+    e = en;
   }
 }
 

@@ -977,6 +977,10 @@ constexpr uint32_t kNoChunk = 0xffffffffu;
 // the long kernel's chunk order: runs of kRun consecutive chunks per wave,
 // kRunBig when the sample is mostly big chunks (general_body)
 constexpr uint64_t kRun = 64, kRunBig = 1;
+#ifndef IXGRX_PRE_T
+#define IXGRX_PRE_T 1
+#endif
+constexpr bool kPreT = IXGRX_PRE_T;  // the long walk's transposed prefix load (gen_pre_t)
 // the coalesced fixed-shape kernel's (fastc_loop)
 constexpr uint32_t kRunC = 2;
 // the span-staged short kernel's (short_span_body)
@@ -1006,6 +1010,56 @@ DEV void gen_pre(const KParams& p, const GDesc& g, int lane, GPre& x) {
   load_prefix<0, 6>(p.base + g.off, Lg, reinterpret_cast<const uint8_t*>(p.tab), x.d);
   const bool short_tail = g.L > (uint32_t)kStreamBase && g.L < (uint32_t)kStreamBase + 32u;
   x.v96 = load16(short_tail, p.base + g.off + kStreamBase, p.zero + 16 * lane);
+}
+
+// The long kernel's prefix load, transposed through LDS: the 64 frames' 6
+// prefix pieces (bytes 0..95) are numbered frame-major, and wave instruction
+// t loads pieces 64t .. 64t+63, i.e. ~11 frames' consecutive pieces, instead
+// of one piece of each of the 64 frames (64 cache lines per instruction,
+// which stalled the L1 on their misses: C3's prefix phase alone ran at ~2.8
+// TB/s). The pieces go to the wave's LDS stash (w.pre, 64 x 96 B) and each
+// lane reads its own frame's row back. Synchronous: the caller uses it where
+// the prefix is waited for at once (the walk without the one-ahead prefetch).
+template <bool BIG>
+DEV void gen_pre_t(const KParams& p, const GDesc& g, int lane, const WaveLds& w, GPre& x) {
+  const bool skip = BIG && wave_all(g.L >= kBigMin || g.L == 0u);
+  const bool short_tail = g.L > (uint32_t)kStreamBase && g.L < (uint32_t)kStreamBase + 32u;
+  x.v96 = load16(short_tail, p.base + g.off + kStreamBase, p.zero + 16 * lane);
+  x.d[0] = x.d[1] = x.d[2] = 0;
+  if (skip) {  // a big chunk loads its prefixes in its rounds (big_chunk)
+#pragma unroll
+    for (int k = 3; k < kPrefixDw; k++) x.d[k] = 0u;
+    return;
+  }
+  w.offlo[lane] = (uint32_t)g.off;
+  w.offhi[lane] = (uint32_t)(g.off >> 32);
+  w.end[lane] = g.L;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  u32x4 v[6];
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    const uint32_t q = 64u * (uint32_t)t + (uint32_t)lane, f = q / 6u, j = q - 6u * f;
+    const uint64_t o = ((uint64_t)w.offhi[f] << 32) | w.offlo[f];
+    v[t] = load16(16u * j < w.end[f], p.base + o + 16u * j, p.zero + 16 * lane);
+  }
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    lds_u32* st = w.pre + 4u * (64u * (uint32_t)t + (uint32_t)lane);  // row f, piece j = dword 24 f + 4 j
+    st[0] = v[t].x; st[1] = v[t].y; st[2] = v[t].z; st[3] = v[t].w;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const lds_u32* row = w.pre + (uint32_t)lane * kPrefixDw;
+#pragma unroll
+  for (int k = 3; k < kPrefixDw; k++) x.d[k] = row[k];
+  // (the stash is read before anything else writes it: the big-chunk path
+  // fills it only inside big_chunk, after this wave's reads)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // ---- big chunks ---------------------------------------------------------
@@ -1774,7 +1828,12 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
   GDesc D1;
   gen_desc<OFFS>(p, c1, lane, D1);
   GPre P0;
-  gen_pre<GATE, BIG>(p, D0, lane, P0);
+  // the walk that waits for each prefix at once takes the transposed load
+  constexpr bool TP = kPreT && MODE == kModeLong && !EARLY && !(LATE_OK && MODE == kModeLong);
+  if (TP)
+    gen_pre_t<BIG>(p, D0, lane, w, P0);
+  else
+    gen_pre<GATE, BIG>(p, D0, lane, P0);
   for (uint32_t j = 0; j < nq; j++) {
     const uint32_t c2 = j + 2 < nq ? q[j + 2] : kNoChunk;
     GDesc D2;
@@ -1783,7 +1842,12 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
     if (EARLY) gen_pre<GATE, BIG>(p, D1, lane, P1);
     constexpr bool LATE = LATE_OK && !EARLY && MODE == kModeLong;
     deferred |= general_chunk<OFFS, MODE, BIG, SM, LATE, DMX>(p, T, c0, lane, w, D0, P0, &D1, &P1);
-    if (!EARLY && !LATE) gen_pre<GATE, BIG>(p, D1, lane, P1);
+    if (!EARLY && !LATE) {
+      if (TP)
+        gen_pre_t<BIG>(p, D1, lane, w, P1);
+      else
+        gen_pre<GATE, BIG>(p, D1, lane, P1);
+    }
     c0 = c1;
     c1 = c2;
     D0 = D1;
