@@ -200,7 +200,7 @@ struct ixg_rx_async_cfg {
 #define IXG_ASYNC_DEF_FRAMES 16384u
 #define IXG_ASYNC_DEF_BYTES (4u << 20)
 #define IXG_ASYNC_DEF_WAIT_US 50u
-#define IXG_ASYNC_DEF_DEPTH 3u
+#define IXG_ASYNC_DEF_DEPTH 2u
 #define IXG_ASYNC_DEF_FLAGS IXG_ASYNC_DIRECT
 
 /* Configure (or re-configure, with nothing pending) the context's

@@ -74,7 +74,7 @@ class AsyncCfg(ctypes.Structure):
 
 
 IXG_ASYNC_DIRECT = 1 << 0
-ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=4 << 20, max_wait_us=50, depth=3, direct=True)
+ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=4 << 20, max_wait_us=50, depth=2, direct=True)
 
 
 class RxFrames(ctypes.Structure):
@@ -255,7 +255,7 @@ class RxEngine:
 
     # ---- the asynchronous host path (ixg_rx_submit_mbufs / ixg_rx_poll) ----
     def async_init(self, batch_frames: int = 16384, batch_bytes: int = 4 << 20, max_wait_us: int = 50,
-                   depth: int = 3, direct: bool = True) -> None:
+                   depth: int = 2, direct: bool = True) -> None:
         c = AsyncCfg(batch_frames, batch_bytes, max_wait_us, depth, IXG_ASYNC_DIRECT if direct else 0)
         _check(self._lib.ixg_rx_async_init(self._ctx, ctypes.byref(c)), "ixg_rx_async_init", self._lib)
 
