@@ -977,10 +977,7 @@ constexpr uint32_t kNoChunk = 0xffffffffu;
 // the long kernel's chunk order: runs of kRun consecutive chunks per wave,
 // kRunBig when the sample is mostly big chunks (general_body)
 constexpr uint64_t kRun = 64, kRunBig = 1;
-#ifndef IXGRX_PRE_T
-#define IXGRX_PRE_T 1
-#endif
-constexpr bool kPreT = IXGRX_PRE_T;  // the long walk's transposed prefix load (gen_pre_t)
+constexpr bool kPreT = true;  // the long walk's transposed prefix load (gen_pre_t)
 // the coalesced fixed-shape kernel's (fastc_loop)
 constexpr uint32_t kRunC = 2;
 // the span-staged short kernel's (short_span_body)
