@@ -3,13 +3,15 @@
  * resident: an echoserver's replies are built by the TX kernel (what
  * tcp_output_packet + ip_send_one + the NIC's checksum offload do), then
  * received back as a loopback batch: RX + PCB demux in one pass (eth_input ..
- * tcp_input's lookup), then the usys descriptors libix consumes
+ * tcp_input's lookup), the rest of the tcp_input head (seqno, ackno, wnd,
+ * tcplen in host order), then the usys descriptors libix consumes
  * (recv_a_pbuf's usys_tcp_recv).
  *
  * Every connection i is ESTABLISHED on the receiving side; its PCB is placed
  * in the flow group and bucket its packets hash to, read off the RX records
  * (IX computes the same at connect time). Checks: every frame is a TCP frame
- * with both checksums verified, every segment demuxes to its own PCB, and
+ * with both checksums verified, every segment demuxes to its own PCB, its
+ * seqno/ackno/wnd/tcplen/ports are the ones the segment was built with, and
  * one USYS_TCP_RECV per segment carries that PCB's handle and cookie.
  *
  * build: gcc -O2 -Iinclude -I/opt/rocm/include examples/ix_echo_pipeline.c \
@@ -103,7 +105,7 @@ int main(void)
 	if ((rc = ixg_tx_set_macs(ctx, smac, dmacs, 4)))
 		return fail("ixg_tx_set_macs", rc);
 
-	void *d_seg, *d_segs, *d_frames, *d_len, *d_rec, *d_dmx, *d_pcbs, *d_ev, *d_idx, *d_cnt;
+	void *d_seg, *d_segs, *d_frames, *d_len, *d_rec, *d_dmx, *d_pcbs, *d_ev, *d_idx, *d_cnt, *d_ext;
 	HIP(hipMalloc(&d_seg, sizeof(seg_buf)));
 	HIP(hipMalloc(&d_segs, sizeof(segs)));
 	HIP(hipMalloc(&d_frames, (size_t)N * SLOT + IXG_TAIL_PAD));
@@ -114,6 +116,7 @@ int main(void)
 	HIP(hipMalloc(&d_ev, N * sizeof(struct ixg_bsys_desc)));
 	HIP(hipMalloc(&d_idx, N * sizeof(uint32_t)));
 	HIP(hipMalloc(&d_cnt, sizeof(uint32_t)));
+	HIP(hipMalloc(&d_ext, N * sizeof(struct ixg_tcp_ext)));
 	HIP(hipMemset(d_frames, 0, (size_t)N * SLOT + IXG_TAIL_PAD));
 	HIP(hipMemcpy(d_seg, seg_buf, sizeof(seg_buf), hipMemcpyHostToDevice));
 	HIP(hipMemcpy(d_segs, segs, sizeof(segs), hipMemcpyHostToDevice));
@@ -160,6 +163,9 @@ int main(void)
 	/* ---- RX + demux in one pass, then the usys descriptors */
 	if ((rc = ixg_rx_demux_batch_dev(ctx, &fr, N, d_rec, d_dmx, NULL)))
 		return fail("ixg_rx_demux_batch_dev", rc);
+	/* the rest of the tcp_input head: what tcp_process reads from its context */
+	if ((rc = ixg_tcp_ext_batch_dev(ctx, &fr, d_rec, N, d_ext, 0, NULL)))
+		return fail("ixg_tcp_ext_batch_dev", rc);
 	static struct ixg_ev_pcb pcbs[N];
 	for (uint32_t i = 0; i < N; i++) {
 		pcbs[i].pcb_idx = 1000u + i;           /* its pcb mempool index */
@@ -179,16 +185,26 @@ int main(void)
 	HIP(hipMemcpy(&cnt, d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
 	HIP(hipMemcpy(ev, d_ev, sizeof(ev), hipMemcpyDeviceToHost));
 	HIP(hipMemcpy(idx, d_idx, sizeof(idx), hipMemcpyDeviceToHost));
-	unsigned own = 0, good_ev = 0;
-	for (uint32_t i = 0; i < N; i++)
+	static struct ixg_tcp_ext ext[N];
+	HIP(hipMemcpy(ext, d_ext, sizeof(ext), hipMemcpyDeviceToHost));
+	unsigned own = 0, good_ev = 0, head_ok = 0;
+	for (uint32_t i = 0; i < N; i++) {
 		own += dmx[i].kind == IXG_D_ACTIVE && dmx[i].id == i;
+		const uint8_t *t = seg_buf + 28u * i;
+		const uint32_t seq = (uint32_t)t[4] << 24 | (uint32_t)t[5] << 16 | (uint32_t)t[6] << 8 | t[7];
+		const uint32_t ack = (uint32_t)t[8] << 24 | (uint32_t)t[9] << 16 | (uint32_t)t[10] << 8 | t[11];
+		head_ok += ext[i].seqno == seq && ext[i].ackno == ack && ext[i].wnd == 0x1000 &&
+			   ext[i].tcplen == SEG - 20 && ext[i].src_port == 7 &&
+			   ext[i].dst_port == ((uint32_t)t[2] << 8 | t[3]);
+	}
 	for (uint32_t k = 0; k < cnt && k < N; k++) {
 		const uint32_t i = idx[k];
 		const uint64_t handle = ((uint64_t)rec[i].fg_id << 48) | (1000u + i);
 		good_ev += ev[k].sysnr == IXG_USYS_TCP_RECV && ev[k].arga == handle && ev[k].argb == pcbs[i].cookie &&
 			   ev[k].argc == iomap + (uint64_t)SLOT * i + 54 && ev[k].argd == SEG - 20;
 	}
-	printf("tx=%u rx_tcp_csum_ok=%u demux_own_pcb=%u usys_tcp_recv=%u/%u\n", N, tcp_ok, own, good_ev, cnt);
+	printf("tx=%u rx_tcp_csum_ok=%u demux_own_pcb=%u tcp_head=%u usys_tcp_recv=%u/%u\n", N, tcp_ok, own, head_ok,
+	       good_ev, cnt);
 	ixg_rx_fini(ctx);
-	return (tcp_ok == N && own == N && good_ev == N && cnt == N) ? 0 : 1;
+	return (tcp_ok == N && own == N && head_ok == N && good_ev == N && cnt == N) ? 0 : 1;
 }

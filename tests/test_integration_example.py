@@ -58,7 +58,7 @@ def test_pipeline_example_builds_and_fails_cleanly_without_gpu(tmp_path):
 def test_pipeline_example_runs_on_gpu(tmp_path):
     r = subprocess.run([_build_pipeline(tmp_path)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert "usys_tcp_recv=4096/4096" in r.stdout
+    assert "usys_tcp_recv=4096/4096" in r.stdout and "tcp_head=4096" in r.stdout
 
 
 def _build_loop(tmp_path):
