@@ -645,3 +645,33 @@ def test_fdir_vs_oracle(kind, layout, engines):
     plain, _ = oracle.rx_trace(tr, KEY, threads=8)
     _diff(eng.batch_trace(tr), plain, f"fdir removed {kind} {layout}")
 
+
+
+@pytest.mark.parametrize("layout", ["stride", "packed"])
+def test_big_kernel_mixed_chunks(layout, engines):
+    """The big-chunk kernel (LONG mode, most chunks big) takes the big chunks
+    of IPv4 ihl 5 frames and flags the rest for the general kernel: chunks
+    with an IPv4-options frame, with a short frame, with an IPv6 frame, with
+    bad checksums, and a partial last chunk, all against the oracle."""
+    rng = np.random.default_rng(0xB16)
+    n_chunks = 96
+    rows = [bytes(r) for r in traces.build_ipv4(rng, 64 * n_chunks, 1514, 6)]
+    rows += [bytes(r) for r in traces.build_ipv4(rng, 37, 1000, 17)]  # partial last chunk (UDP)
+    frames = list(rows)
+    opt = [bytes(r) for r in traces.build_ipv4(rng, 8, 1514, 6, ihl=7)]
+    for k in range(8):  # chunks 10..17: one IPv4-options frame each (big, not ihl 5)
+        frames[64 * (10 + k) + 5 * k] = opt[k]
+    for k in range(8):  # chunks 20..27: one short frame each (not big)
+        frames[64 * (20 + k) + 3] = bytes(traces.build_ipv4(rng, 1, 60, 6)[0])
+    for k in range(4):  # chunks 30..33: an IPv6 frame
+        frames[64 * (30 + k) + 9] = mg.ipv6(payload=b"z" * 1400)
+    for k in range(8):  # chunks 40..47: bad IP / L4 checksums
+        f = bytearray(frames[64 * (40 + k) + k])
+        f[24 if k % 2 else 60] ^= 1
+        frames[64 * (40 + k) + k] = bytes(f)
+    tr = traces.pack(frames, stride=1516) if layout == "stride" else traces.pack(frames)
+    for flags in (0, ixgrx.IXG_F_IPV6):
+        rec, cs = engines(flags=flags).batch_trace(tr, want_csum=True)
+        er, ec = oracle.rx_trace(tr, KEY, flags=flags, threads=8)
+        _diff(rec, er, f"big mixed {layout} flags={flags}")
+        assert (cs == ec).all()
