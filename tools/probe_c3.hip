@@ -179,10 +179,10 @@ __global__ void __launch_bounds__(256) k_lds(const uint8_t* base, const uint64_t
 
 extern "C" const char* p3_name(int w) {
   static const char* nm[] = {"reg_u4", "reg_u8", "reg_u16", "lds_4k", "reg2_u8", "reg2_u16", "reg2_u24",
-                             "reg3_u16_c4", "reg3_u16_c16", "reg3_u16_c64", "reg3_u8_c4"};
+                             "reg3_u16_c4", "reg3_u16_c16", "reg3_u16_c64", "reg3_u8_c4", "reg3_u8_c1", "reg3_u8_c2"};
   return nm[w];
 }
-extern "C" int p3_count(void) { return 11; }
+extern "C" int p3_count(void) { return 13; }
 extern "C" int p3_launch(int which, const void* base, const void* off, const void* len, void* out, uint32_t n,
                          const void* zero, uint32_t grid, void* stream) {
   hipStream_t s = (hipStream_t)stream;
@@ -197,6 +197,8 @@ extern "C" int p3_launch(int which, const void* base, const void* off, const voi
   if (which == 5) hipLaunchKernelGGL(k_reg2<16>, dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 6) hipLaunchKernelGGL(k_reg2<24>, dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 7) hipLaunchKernelGGL((k_reg3<16, 4>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
+  if (which == 11) hipLaunchKernelGGL((k_reg3<8, 1>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
+  if (which == 12) hipLaunchKernelGGL((k_reg3<8, 2>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 8) hipLaunchKernelGGL((k_reg3<16, 16>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 9) hipLaunchKernelGGL((k_reg3<16, 64>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);
   if (which == 10) hipLaunchKernelGGL((k_reg3<8, 4>), dim3(grid), dim3(256), 0, s, bp, op, lp, o, n);

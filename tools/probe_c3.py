@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Memory ceiling of C3's byte pattern (diagnostic): tools/probe_c3.hip's
+"""Memory ceiling of C3's (or argv[1]'s workload's) byte pattern (diagnostic): tools/probe_c3.hip's
 whole-span reads next to the product's C3 launch on the same buffers."""
 import ctypes
 import json
@@ -23,11 +23,12 @@ def main():
                                                                         ctypes.c_uint32, ctypes.c_void_p]
     lib.p3_name.restype = ctypes.c_char_p
     dev = torch.device("cuda:0")
-    wl = bench.Workload("c3", seed=0x1B0002, dev=dev)
+    wname = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    wl = bench.Workload(wname, seed=0x1B0002, dev=dev)
     zero = torch.zeros(4096, dtype=torch.uint8, device=dev)
     out = torch.empty((wl.n, 16), dtype=torch.uint8, device=dev)
     s = torch.cuda.current_stream()
-    eng = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, 128, 0, 0), device=0)
+    eng = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, 128, 0, wl.flags), device=0)
     span = int(wl.off[-1].item()) + int(wl.len[-1].item())
     res = {}
 
@@ -50,7 +51,7 @@ def main():
                 t = timeit(lambda: lib.p3_launch(w, wl.blob.data_ptr(), wl.off.data_ptr(), wl.len.data_ptr(),
                                                  out.data_ptr(), wl.n, zero.data_ptr(), g, s.cuda_stream))
                 res.setdefault(name, []).append(t)
-    print(json.dumps({"span_bytes": span, "n": wl.n,
+    print(json.dumps({"workload": wname, "span_bytes": span, "n": wl.n,
                       "ms": {k: round(min(v), 4) for k, v in res.items()},
                       "tbps_span_read": {k: round(span / (min(v) * 1e-3) / 1e12, 2) for k, v in res.items()}}))
     eng.close()
