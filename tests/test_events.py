@@ -126,6 +126,39 @@ def test_gpu_pipeline_vs_oracle(eng, n):
 
 
 @pytest.mark.gpu
+def test_gpu_back_to_back_launches(eng):
+    """Launches queued on one stream without a sync in between, over a batch
+    of 17K chunks (the per-chunk and per-group scratch counts and bases are
+    rewritten by every launch): every launch's output equals the oracle's."""
+    import torch
+    n = 1_100_003
+    tr, rec, dmx, pcbs = _imix_pipeline(n, 0x7E0300)
+    io = 0x7F0000000000
+    eev, eidx, _ = oracle.ev_batch(tr.blob, tr.off, 0, rec, dmx, pcbs, io, 0)
+    dev = torch.device("cuda:0")
+    tb = torch.from_numpy(np.concatenate([tr.blob, np.zeros(64, np.uint8)])).to(dev)
+    to = torch.from_numpy(np.ascontiguousarray(tr.off).view(np.int64)).to(dev)
+    trr = torch.from_numpy(np.ascontiguousarray(rec).view(np.uint8).reshape(n, 16)).to(dev)
+    td = torch.from_numpy(np.ascontiguousarray(dmx).view(np.uint8).reshape(n, 8)).to(dev)
+    tp = torch.from_numpy(pcbs.view(np.uint8)).to(dev)
+    outs = []
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(3):
+        ev = torch.zeros((n, 40), dtype=torch.uint8, device=dev)
+        fi = torch.zeros(n, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        events.batch_dev(eng, tb.data_ptr(), to.data_ptr(), 0, trr.data_ptr(), td.data_ptr(), tp.data_ptr(),
+                         len(pcbs), n, io, 0, ev.data_ptr(), fi.data_ptr(), cnt.data_ptr(), s)
+        outs.append((ev, fi, cnt))
+    torch.cuda.synchronize()
+    for ev, fi, cnt in outs:
+        k = int(cnt.item())
+        assert k == len(eev)
+        assert (ev[:k].cpu().numpy().reshape(-1).view(events.EV_DTYPE).view(np.uint8) == eev.view(np.uint8)).all()
+        assert (fi[:k].cpu().numpy().astype(np.uint32) == eidx).all()
+
+
+@pytest.mark.gpu
 def test_gpu_stride_layout_no_demux(eng):
     tr = traces.make_trace("tcp64", 3000, seed=0x7E0200)
     rec, _ = oracle.rx_trace(tr, traces.RSS_KEY)
