@@ -87,6 +87,29 @@ def alg_bytes(tr, flags: int = 0) -> np.ndarray:
     return rd + desc + 16
 
 
+def line_floor_bytes(tr, flags: int = 0, line: int = 128) -> float:
+    """The bytes per frame a memory system that fetches whole `line`-byte
+    lines must move: the distinct lines of the batch that hold a byte the
+    path reads (frame bytes [12, alg_bytes' read end), as in alg_bytes),
+    plus the descriptor and the record. For packed batches whose frames the
+    reference reads only in part (C5 in reference semantics: IPv6 frames
+    dropped on the Ethernet type) this is the reachable floor; the 8(d)
+    bytes count only the bytes read."""
+    offs = tr.offsets().astype(np.int64)
+    b = tr.blob
+    et = (b[offs + 12].astype(np.int64) << 8) | b[offs + 13]
+    v4 = (b[offs + 16].astype(np.int64) << 8) | b[offs + 17]
+    v6 = (b[offs + 18].astype(np.int64) << 8) | b[offs + 19]
+    rd = np.minimum(np.where(et == 0x86DD, 54 + v6 if flags & 2 else 14, 14 + v4), tr.len.astype(np.int64))
+    lo, hi = (offs + 12) // line, (offs + np.maximum(rd, 13) - 1) // line
+    mark = np.zeros(int(hi.max()) + 2, dtype=np.int64)
+    np.add.at(mark, lo, 1)
+    np.add.at(mark, hi + 1, -1)
+    lines = int((np.cumsum(mark) > 0).sum())
+    desc = 2 + (8 if tr.off is not None else 0)
+    return lines * line / tr.n + desc + 16
+
+
 class Workload:
     """A batch of n frames on `dev`, tiled from `pool` distinct frames."""
 
@@ -305,13 +328,13 @@ def parity_leg(checks, key) -> dict:
                 np.array_equal(out[o:o + L], eo[o:o + L]) for o, L in zip(segs["out_off"].astype(np.int64), el))
             res["tx_" + kind] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
         else:
-            _, pool, tabs, rec, dmx, tiled = c
+            _, name, pool, tabs, rec, dmx, tiled = c
             er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
             exp = oracle.demux_batch(tabs.nfg, tabs.active_start, tabs.active, tabs.tw_start, tabs.tw, tabs.listen,
                                      0, pool.blob, pool.off, pool.len, pool.stride, er)
             ok = tiled and np.array_equal(rec, er) and np.array_equal(dmx, exp)
-            res["demux"] = "ok" if ok else "MISMATCH"
-            res["demux_kinds"] = {demux.KINDS[int(v)]: int(n) for v, n in zip(*np.unique(exp[:, 4], return_counts=True))}
+            res[name] = "ok" if ok else "MISMATCH"
+            res[name + "_kinds"] = {demux.KINDS[int(v)]: int(n) for v, n in zip(*np.unique(exp[:, 4], return_counts=True))}
     return res
 
 
@@ -380,11 +403,18 @@ def copy_overlapped(wl, engs, pieces=16, reps=3):
 
 def demux_line(dev, key, steps: int, rank: int, eng_for):
     """PCB demux over C2's shape: 16M 64-B TCP frames tiled
-    from 2^16 distinct connections, every one ESTABLISHED (the echoserver
-    case), 1% extra TIME-WAIT entries and one listener. Two forms, each a
-    step = one launch: the fused RX + demux (ixg_rx_demux_batch_dev: the
-    lookup runs in the RX kernels from the parse state) and the separate
-    demux pass over frames + records already in HBM (ixg_demux_batch_dev)."""
+    from 2^16 distinct connections. Two forms, each a step = one launch: the
+    fused RX + demux (ixg_rx_demux_batch_dev: the lookup runs in the RX
+    kernels from the parse state) and the separate demux pass over frames +
+    records already in HBM (ixg_demux_batch_dev). Three table sets:
+    `established` (every connection ESTABLISHED, the echoserver case; 1 %
+    extra TIME-WAIT entries of other connections and one listener, which no
+    frame reaches), `mixed` (90 % of the connections active, 5 % in
+    TIME-WAIT with their own tuple, 5 % unknown, which the listen list takes:
+    a non-empty list hands an unmatched segment to its last entry,
+    tcp_in.c:317-323) and `mixed_nolisten` (the same without listeners: the
+    unknown 5 % get RESET, tcp_in.c:500-510). Every outcome of the lookup
+    occurs in one of them, each checked against the oracle."""
     import torch
     from ix_amd import demux
     wl = Workload("c2", seed=0x1BD000 + 97 * rank, dev=dev, pool=1 << 16)
@@ -399,8 +429,11 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
     tw["id"] += 1 << 20
     tw["remote_port"] ^= 1  # TIME-WAIT entries of other (closed) connections
     lis = np.array([(0, 80, 0, 7, 0)], dtype=demux.LISTEN_DTYPE)
-    tabs = demux.DemuxTables.build(cfg, keys, tw, lis)
-    demux.load(eng, tabs)
+    u = np.random.default_rng(2).random(keys.size)
+    tabsets = {"established": demux.DemuxTables.build(cfg, keys, tw, lis),
+               "mixed": demux.DemuxTables.build(cfg, keys[u < 0.90], keys[(u >= 0.90) & (u < 0.95)], lis),
+               "mixed_nolisten": demux.DemuxTables.build(cfg, keys[u < 0.90], keys[(u >= 0.90) & (u < 0.95)],
+                                                         np.zeros(0, demux.LISTEN_DTYPE))}
     out = torch.empty((wl.n, 8), dtype=torch.uint8, device=dev)
     out2 = torch.empty((wl.n, 8), dtype=torch.uint8, device=dev)
     rec2 = torch.empty((wl.n, 16), dtype=torch.uint8, device=dev)
@@ -425,12 +458,6 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
             b.record(stream)
         torch.cuda.synchronize()
         return time.perf_counter() - t0, float(np.mean([a.elapsed_time(b) * 1e-3 for a, b in ev]))
-    el, k = timed(separate)
-    elf, kf = timed(fused)
-    v = out.view(wl.reps, -1, 8)
-    tiled = bool(torch.equal(v, v[:1].expand(wl.reps, -1, -1))) and bool(torch.equal(out, out2)) and \
-        bool(torch.equal(rec2, wl.out))
-    check = ("demux", pool, tabs, wl.out.view(wl.reps, -1, 16)[0].cpu().numpy(), v[0].cpu().numpy(), tiled)
     # separate pass, algorithmic bytes per frame: the record (16), the header
     # bytes the lookup reads (byte 14 + the 12 tuple bytes), the bucket bounds
     # (8), the entries compared up to the match (16 each, here ~1 per bucket)
@@ -438,15 +465,33 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
     # reads are L2 / Infinity-Cache resident: 64K connections = 1 MiB).
     alg = 16 + 13 + 8 + 16 * 1.0 + 8
     algf = 72 + 8
-    return {"workload": "PCB demux over C2: 16M x 64B TCP frames, 65536 established connections, 1% TIME-WAIT, "
-                        "1 listener",
-            "fused": {"kernel": "RX kernels with the lookup fused (ixg_rx_demux_batch_dev)",
-                      "mpps": round(wl.n * steps / elf / 1e6, 2), "kernel_ms_avg": round(kf * 1e3, 4),
-                      "alg_bytes_per_pkt": algf, "roofline_frac": round(algf * wl.n / kf / 1e9 / PEAK_HBM_GBPS, 4)},
-            "separate": {"kernel": "ixg_demux_s over RX records in HBM (ixg_demux_batch_dev)",
-                         "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
-                         "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4)},
-            "parity": "tiled-consistent" if check[-1] else "MISMATCH"}, check
+    res, checks = {"workload": "PCB demux over C2: 16M x 64B TCP frames, 65536 connections; table sets "
+                               "established (all ESTABLISHED, 1% other TIME-WAIT entries, 1 listener), mixed "
+                               "(90% active, 5% TIME-WAIT, 5% unknown -> listen list), mixed_nolisten (unknown "
+                               "-> RESET)"}, []
+    for name, tabs in tabsets.items():
+        demux.load(eng, tabs)
+        el, k = timed(separate)
+        elf, kf = timed(fused)
+        v = out.view(wl.reps, -1, 8)
+        tiled = bool(torch.equal(v, v[:1].expand(wl.reps, -1, -1))) and bool(torch.equal(out, out2)) and \
+            bool(torch.equal(rec2, wl.out))
+        checks.append(("demux", "demux" if name == "established" else "demux_" + name, pool, tabs,
+                       wl.out.view(wl.reps, -1, 16)[0].cpu().numpy(), v[0].cpu().numpy(), tiled))
+        line = {"fused": {"kernel": "RX kernels with the lookup fused (ixg_rx_demux_batch_dev)",
+                          "mpps": round(wl.n * steps / elf / 1e6, 2), "kernel_ms_avg": round(kf * 1e3, 4),
+                          "alg_bytes_per_pkt": algf,
+                          "roofline_frac": round(algf * wl.n / kf / 1e9 / PEAK_HBM_GBPS, 4)},
+                "separate": {"kernel": "ixg_demux_s over RX records in HBM (ixg_demux_batch_dev)",
+                             "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
+                             "alg_bytes_per_pkt": alg,
+                             "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4)},
+                "parity": "tiled-consistent" if tiled else "MISMATCH"}
+        if name == "established":
+            res.update(line)
+        else:
+            res[name] = line
+    return res, checks
 
 
 def events_line(dev, key, steps: int, rank: int, eng_for):
@@ -874,6 +919,56 @@ def strong_leg(dev, run_slice, dist, world: int, rank: int, n_total: int = C4_FR
     return res, check
 
 
+def summary(res: dict) -> dict:
+    """Every line of the run in one compact object, the last key of the JSON
+    line, so a reader that keeps only the line's tail (the driver's record
+    keeps ~2 KB) still sees each config's roofline fraction, kernel time per
+    launch, rate and parity."""
+    def ent(frac, ms, mpps, par):
+        return {"frac": None if frac is None else round(frac, 4), "kernel_ms": None if ms is None else round(ms, 4),
+                "mpps": None if mpps is None else round(mpps, 1), "parity": par}
+    out = {"c2": ent(res["roofline"]["frac"], res["roofline"]["kernel_ms_avg"], res["value"], res.get("parity"))}
+    if "bad_csum" in res:
+        b = res["bad_csum"]
+        out["c2b"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+    if "secondary" in res:
+        b = res["secondary"]
+        out["c4"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+    for name, b in res.get("lines", {}).items():
+        out[name] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+    if "c4_strong" in res:
+        b = res["c4_strong"]
+        out["c4_strong"] = ent(b["roofline_frac_per_gpu"], b["kernel_ms"], b["mpps_device_resident"], b.get("parity"))
+    if "demux" in res:
+        d = res["demux"]
+        out["demux_fused"] = ent(d["fused"]["roofline_frac"], d["fused"]["kernel_ms_avg"], d["fused"]["mpps"],
+                                 d["parity"])
+        out["demux_sep"] = ent(d["separate"]["roofline_frac"], d["separate"]["kernel_ms_avg"], d["separate"]["mpps"],
+                               d["parity"])
+        for name in ("mixed", "mixed_nolisten"):
+            if name in d:
+                m = d[name]
+                out["demux_" + name] = ent(m["fused"]["roofline_frac"], m["fused"]["kernel_ms_avg"],
+                                           m["fused"]["mpps"], m["parity"])
+                out["demux_" + name]["kinds"] = m.get("kinds")
+    if "events" in res:
+        b = res["events"]
+        out["events"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mevents_per_s"], b["parity"])
+    if "tcpx" in res:
+        b = res["tcpx"]
+        out["tcpx"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+    for kind, b in res.get("tx", {}).items():
+        out["tx_" + kind] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+    hp = res.get("host_path", {})
+    if "loop" in hp:
+        lp = hp["loop"]
+        out["host_path"] = {k.replace("threads", "t"): lp[k].get("mpps") for k in lp}
+        out["host_path"]["parity"] = hp.get("parity")
+    if "cpu_baseline" in res:
+        out["cpu_baseline_mpps"] = res["cpu_baseline"]["value"]
+    return out
+
+
 def load_traffic(workload: str):
     """HBM bytes per launch from the committed rocprofv3 --pmc summary, or None."""
     p = os.path.join(ROOT, "profiles", "traffic.json")
@@ -1033,6 +1128,11 @@ def main():
             "kernel_ms_avg": round(kea * 1e3, 4), "kernel_ms_min": round(kem * 1e3, 4),
             "alg_bytes_per_pkt": round(wle.bytes_per_pkt, 1), "traffic": tr_e, "kernel": kernels(wle),
             "parity": "tiled-consistent" if te else "MISMATCH"}
+        if wle.off is not None:
+            # the same launch against the bytes whole 128-B lines make it move
+            fl = line_floor_bytes(wle.pool, wle.flags)
+            res["lines"][name]["line_floor_bytes_per_pkt"] = round(fl, 1)
+            res["lines"][name]["frac_vs_line_floor"] = round(fl * wle.n / kea / 1e9 / PEAK_HBM_GBPS, 4)
         wl = wle
     if not args.no_strong and args.workload == "c2":
         del wl
@@ -1054,7 +1154,7 @@ def main():
         del wl
         torch.cuda.empty_cache()
         res["demux"], dchk = demux_line(dev, key, max(5, args.steps // 2), rank, engine)
-        checks.append(dchk)
+        checks.extend(dchk)
         wl = None
     if not args.no_demux and args.workload == "c2":
         torch.cuda.empty_cache()
@@ -1099,8 +1199,6 @@ def main():
             res["cpu_baseline"] = cpu_baseline(ptr, pflags, key, args.cpu_seconds, threads, pname)
         par = parity_leg(checks, key)
         res["parity_vs_oracle"] = par
-        if "cpu_baseline" in res:
-            res["cpu_baseline"]["parity_vs_oracle"] = par
         res["parity"] = par[wl_name]
         if "secondary" in res:
             res["secondary"]["parity"] = par[args.secondary]
@@ -1111,6 +1209,10 @@ def main():
         if "demux" in res:
             res["demux"]["parity"] = par["demux"]
             res["demux"]["kinds"] = par["demux_kinds"]
+            for name in ("mixed", "mixed_nolisten"):
+                if name in res["demux"]:
+                    res["demux"][name]["parity"] = par["demux_" + name]
+                    res["demux"][name]["kinds"] = par["demux_" + name + "_kinds"]
         if "host_path" in res and "hostpath" in par:
             res["host_path"]["parity"] = par["hostpath"]
         if "mbuf_path" in res:
@@ -1124,6 +1226,7 @@ def main():
         if "bad_csum" in res:
             res["bad_csum"]["parity"] = par["c2b"]
     if rank == 0:
+        res["summary"] = summary(res)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -213,7 +213,11 @@ int ixg_rx_async_init(void *ctx, const struct ixg_rx_async_cfg *cfg);
  * (< n when every batch of the ring is in flight or unpolled: poll, then
  * submit the rest; the caller keeps those mbufs, as IX keeps frames queued
  * on its RX queue) or -errno. The library keeps the mbuf pointers until poll
- * returns them and never writes to or frees an mbuf. */
+ * returns them and never writes to or frees an mbuf. A launch that fails
+ * after frames of this call were accepted does not undo them: the call
+ * returns the count, the frames stay in the open batch (launched again by a
+ * later submit, flush or poll), and the next submit, poll or flush returns
+ * the launch's -errno once. */
 int ixg_rx_submit_mbufs(void *ctx, void *const *mbufs, uint32_t n);
 
 /* Launch the open batch now (e.g. before idling). 0 or -errno. */
@@ -278,10 +282,13 @@ struct ixg_fdir_filter {
  * filters steer to (the queue of the CPU that connected). The table lives in
  * device memory and the kernels read it at run time, so a launch captured in
  * a HIP graph sees the current filters, unless the set grew past every
- * earlier one (the table then moves: capture again). Not concurrently with
- * this context's launches: the call synchronizes the context's own stream
- * only, so the caller finishes its launches on other streams first. 0 or
- * -errno. */
+ * earlier one (the table then moves: capture again). Before it writes the
+ * table the call waits for every launch the library made for this context:
+ * its own stream, the pipelined mbuf path, and the asynchronous ring, whose
+ * open batch it launches first, so frames submitted before the call are
+ * matched against the filters in force when they were submitted. The
+ * caller's own launches on its streams (ixg_rx_batch_dev and graphs) it
+ * cannot see: finish those first. 0 or -errno. */
 int ixg_rx_set_fdir(void *ctx, const struct ixg_fdir_filter *filters, uint32_t n, uint16_t cpu_id);
 
 /* How the context's RX launches divide a batch between the kernels

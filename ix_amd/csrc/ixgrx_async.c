@@ -48,6 +48,9 @@ struct ixg_async {
 	uint32_t head;       /* oldest batch not yet fully polled */
 	uint32_t tail;       /* next batch to open */
 	uint32_t count;      /* batches in the ring that are not FREE */
+	int err;             /* a launch that failed after submit had accepted
+	                        frames: reported (and cleared) by the next
+	                        submit / poll / flush; the batch stays OPEN */
 	size_t bytes_cap;    /* gathered-bytes capacity of a batch */
 	struct ixg_abatch b[IXG_ASYNC_MAX_DEPTH];
 };
@@ -219,6 +222,11 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 	}
 	HIPCHK(hipSetDevice(c->device));
 	struct ixg_async *a = c->async;
+	if (a->err) {
+		const int e = a->err;
+		a->err = 0;
+		return e;
+	}
 	const uint64_t t = now_ns();
 	uint32_t done = 0;
 	while (done < n) {
@@ -249,8 +257,14 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 		done += m;
 		if (due(a, b, t)) {
 			int rc = launch_open(c, a);
-			if (rc)
-				return rc;
+			if (rc) {
+				/* the accepted frames stay in the OPEN batch (owned by the
+				 * library until poll returns them; a later flush, submit or
+				 * poll launches it again): report the count now and the
+				 * error on the next call */
+				a->err = rc;
+				break;
+			}
 		}
 	}
 	return (int)done;
@@ -264,7 +278,28 @@ int ixg_rx_flush(void *vctx)
 	if (!c->async)
 		return 0;
 	HIPCHK(hipSetDevice(c->device));
-	return launch_open(c, c->async);
+	struct ixg_async *a = c->async;
+	if (a->err) {
+		const int e = a->err;
+		a->err = 0;
+		return e;
+	}
+	return launch_open(c, a);
+}
+
+int ixg_async_quiesce(struct ixg_ctx *c)
+{
+	struct ixg_async *a = c->async;
+	if (!a || !a->count)
+		return 0;
+	/* the OPEN batch goes now, with the state its frames were submitted under */
+	int rc = launch_open(c, a);
+	if (rc)
+		return rc;
+	for (uint32_t k = 0, i = a->head; k < a->count; k++, i = (i + 1) % a->cfg.depth)
+		if (a->b[i].state == AS_INFLIGHT)
+			HIPCHK(hipEventSynchronize(a->b[i].done));
+	return 0;
 }
 
 int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max, int wait)
@@ -273,6 +308,11 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 	if (!c || (max && (!mbufs || !recs)))
 		return -EINVAL;
 	struct ixg_async *a = c->async;
+	if (a && a->err) {
+		const int e = a->err;
+		a->err = 0;
+		return e;
+	}
 	if (!a || !a->count || !max)
 		return 0;
 	HIPCHK(hipSetDevice(c->device));

@@ -167,5 +167,8 @@ IXG_INTERNAL int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, cons
 
 /* ixgrx_async.c */
 IXG_INTERNAL void ixg_async_free(struct ixg_ctx *c);
+/* launch the OPEN asynchronous batch and wait for every batch in flight
+ * (their kernels read the context's device tables: ixg_rx_set_fdir) */
+IXG_INTERNAL int ixg_async_quiesce(struct ixg_ctx *c);
 
 #endif

@@ -319,7 +319,21 @@ int ixg_rx_set_fdir(void *vctx, const struct ixg_fdir_filter *f, uint32_t n, uin
 	if (!c || (n && !f) || n > (1u << 24) || IXG_ETH_MAX_TOTAL_FG + (uint32_t)cpu_id > 0xfffeu)
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
+	/* every launch of this context that may read the table finishes first:
+	 * the synchronous paths' stream, the pipelined mbuf path's stages, and
+	 * the asynchronous ring (its OPEN batch is launched first, so frames
+	 * submitted before this call are matched against the filters they were
+	 * submitted under, as frames the NIC received before the filter was
+	 * installed) */
 	HIPCHK(hipStreamSynchronize(c->stream));
+	for (int k = 0; k < IXG_SLOTS; k++)
+		if (c->slot[k].stream)
+			HIPCHK(hipStreamSynchronize(c->slot[k].stream));
+	{
+		const int rc = ixg_async_quiesce(c);
+		if (rc)
+			return rc;
+	}
 	/* open addressing, load factor <= 1/2, linear probing; duplicates kept
 	 * once (a perfect filter matches or not) */
 	uint32_t slots = 16;

@@ -37,6 +37,7 @@ struct op {
 	size_t n;
 	int val;
 	struct ixg_kparams p;
+	uint64_t fdir_sum; /* OP_RX: the flow-director table when launched */
 	struct fevent *ev;
 	struct op *next;
 };
@@ -52,6 +53,22 @@ struct fevent {
 
 static struct ixg_rx_cfg g_cfg;
 static unsigned long g_launches;
+static int g_fail_launches;      /* the next this many RX launches fail */
+static unsigned long g_fdir_stale; /* RX launches that ran after their table changed */
+void fakehip_fail_launches(int k) { g_fail_launches = k; }
+unsigned long fakehip_fdir_stale(void) { return g_fdir_stale; }
+
+/* FNV-1a over the flow-director table a launch reads (header + slots) */
+static uint64_t fdir_sum(const uint32_t *t)
+{
+	if (!t)
+		return 0;
+	const size_t words = 4u * ((t[0] ? (size_t)t[0] + 1u : 0u) + 1u);
+	uint64_t h = 1469598103934665603ull;
+	for (size_t i = 0; i < words; i++)
+		h = (h ^ t[i]) * 1099511628211ull;
+	return h;
+}
 
 /* memory the device can reach: allocations and registered host ranges */
 #define MAXR 4096
@@ -112,6 +129,10 @@ static void run_op(struct op *o)
 				abort();
 			g_inplace += r == 2;
 		}
+		/* a kernel reads the table when it runs: it must still be the one
+		 * in force when the launch was made */
+		if (fdir_sum(o->p.fdir) != o->fdir_sum)
+			g_fdir_stale++;
 		struct ixg_rx_cfg c = g_cfg;
 		ixgo_rx_batch(&c, o->p.base, o->p.off, o->p.len, o->p.stride, o->p.n, o->p.out, o->p.csum, 1,
 			      IXGO_HASH_TABLE, IXGO_WORK_FULL);
@@ -321,8 +342,13 @@ hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int f)
 int ixgrx_launch(const void *params, uint32_t ncu, void *stream)
 {
 	(void)ncu;
+	if (g_fail_launches > 0) {
+		g_fail_launches--;
+		return -1;
+	}
 	struct op *o = new_op(OP_RX);
 	memcpy(&o->p, params, sizeof(o->p));
+	o->fdir_sum = fdir_sum(o->p.fdir);
 	push((hipStream_t)stream, o);
 	return 0;
 }

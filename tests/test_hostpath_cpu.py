@@ -232,3 +232,63 @@ def test_async_zero_copy(fake, kind):
             eng.unregister_memory(arena.ctypes.data)
     finally:
         eng.close()
+
+
+def test_set_fdir_waits_for_async_batches(fake):
+    """ixg_rx_set_fdir from IX's connect path while the run loop has batches
+    in flight: the open batch is launched first and every batch
+    in flight finishes before the table is rewritten, so no launch reads a
+    table other than the one in force when it was made."""
+    fake.lib.fakehip_fdir_stale.restype = ctypes.c_ulong
+    tr, arena, ptrs = _mbufs("tcp64", 200, seed=31)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=64, batch_bytes=1 << 20, max_wait_us=10000000, depth=4)
+        s0, n0 = fake.lib.fakehip_fdir_stale(), fake.lib.fakehip_launches()
+        assert eng.submit_mbufs(ptrs[:64]) == 64       # launched, in flight
+        assert eng.submit_mbufs(ptrs[64:94]) == 30     # open
+        assert fake.lib.fakehip_launches() == n0       # nothing has run yet
+        eng.set_fdir(np.array([(0x0a000001, 0x0a000002, 40000, 80)], dtype=ixgrx.FDIR_DTYPE), cpu_id=3)
+        assert fake.lib.fakehip_launches() - n0 == 2   # the open batch went, both ran
+        assert eng.submit_mbufs(ptrs[94:200]) == 106
+        m, r = eng.poll(1000, wait=True)
+        while eng.pending():
+            m2, r2 = eng.poll(1000, wait=True)
+            m, r = np.concatenate([m, m2]), np.concatenate([r, r2])
+        eng.set_fdir(None, cpu_id=0)
+        assert fake.lib.fakehip_fdir_stale() == s0
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+
+
+def test_submit_launch_failure_keeps_accepted_frames(fake):
+    """A launch that fails after submit accepted frames: submit
+    returns the count it took, the next call reports the error once, and the
+    frames stay in the open batch, launched again later and returned by poll
+    in order, exactly once."""
+    tr, arena, ptrs = _mbufs("imix", 200, seed=32)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=64, batch_bytes=1 << 20, max_wait_us=10000000, depth=2)
+        n0 = fake.lib.fakehip_launches()
+        fake.lib.fakehip_fail_launches(1)
+        assert eng.submit_mbufs(ptrs[:100]) == 64      # the batch filled, its launch failed
+        assert eng.pending() == 64
+        with pytest.raises(RuntimeError, match="ixg_rx_submit_mbufs"):
+            eng.submit_mbufs(ptrs[64:100])           # the error, once
+        m, r = eng.poll(1000, wait=True)             # launches the open batch again
+        assert fake.lib.fakehip_launches() - n0 == 1
+        assert np.array_equal(m, ptrs[:64])
+        fake.lib.fakehip_fail_launches(1)
+        assert eng.submit_mbufs(ptrs[64:100]) == 36
+        with pytest.raises(RuntimeError, match="ixg_rx_flush"):
+            eng.flush()                              # its launch fails: reported by flush itself
+        assert eng.pending() == 36
+        m2, r2 = eng.poll(1000, wait=True)
+        assert np.array_equal(m2, ptrs[64:100]) and eng.pending() == 0
+    finally:
+        eng.close()
+    exp = _expect(ptrs[:100])
+    assert np.array_equal(np.concatenate([r, r2]).view(np.uint8).reshape(-1, 16), exp)
