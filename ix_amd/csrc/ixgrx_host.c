@@ -419,6 +419,22 @@ int ixg_rx_set_split(void *vctx, uint32_t split)
 	return 0;
 }
 
+int ixg_rx_launch_info(void *vctx, uint32_t info[3])
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !info)
+		return -EINVAL;
+	HIPCHK(hipSetDevice(c->device));
+	HIPCHK(hipStreamSynchronize(c->stream));
+	uint32_t w[IXG_PRESENT_WORDS];
+	HIPCHK(hipMemcpy(w, c->ds.d_present, sizeof(w), hipMemcpyDeviceToHost));
+	const int ran = c->ds.epoch != 0 && w[0] == c->ds.epoch;
+	info[0] = ran ? w[3] : 0xffffffffu;
+	info[1] = c->ds.epoch != 0 && w[7] == c->ds.epoch;
+	info[2] = ran && w[6] != 0;
+	return 0;
+}
+
 static int launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *off, const uint16_t *len,
 		  uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum, hipStream_t s)
 {

@@ -1876,7 +1876,11 @@ DEV void general_body(const KParams& p) {
   // a block with no deferred chunk exits before staging the tables (the
   // common case behind the fixed-shape kernel: 64 B frames)
   const uint32_t mode = launch_mode(p);
-  const bool all = CLS == IXG_CLS_SHORT ? mode == IXG_MODE_SHORT : (p.defer == nullptr || mode == IXG_MODE_LONG);
+  // (LONG mode behind the ring kernel, which ran when present[7] holds the
+  // launch's epoch: only the chunks it flagged)
+  const bool all = CLS == IXG_CLS_SHORT
+                       ? mode == IXG_MODE_SHORT
+                       : (p.defer == nullptr || (mode == IXG_MODE_LONG && !(p.ring && p.present[7] == p.epoch)));
   // (p.present is only read when the flags are in use: it is null with
   // p.defer when the general kernel runs alone)
   if (!all) {
@@ -2199,6 +2203,352 @@ IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
 IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
 
 
+// ---- the ring kernel (C3: long chunks of packed batches) --------------------
+// One 1024-thread block per CU takes a contiguous range of chunks. Wave 0 is
+// the loader: for each chunk in order it copies the chunk's descriptor rows
+// (64 u64 offsets + 64 u16 lengths, one 1 KiB header slot) and its span of
+// frame bytes (floor16(first offset) .. last frame's end, whole 1 KiB slots)
+// HBM -> LDS with buffer_load ... lds (no VGPRs, the out-of-range part of a
+// piece reads 0) into a block-wide ring of 1 KiB slots, one chunk after the
+// other, as far ahead as the ring allows. The other 15 waves are consumers:
+// each takes the next chunk in order (an LDS ticket), waits until the loader
+// has published it landed, reads its frames' 96-byte prefixes and sums their
+// L4 tails [96, segment end) out of the ring (16-lane groups per frame,
+// medium segments first), gives the chunk's slots back, and only then parses
+// from registers and stores the records. The ring turns the walk's per-wave
+// HBM round trips (prefix, then 2-4 streaming rounds per chunk, each waiting
+// out the miss latency at 2 waves per SIMD) into one sequential stream per
+// CU with ~32 KiB always in flight.
+//
+// Protocol (all in LDS): queue entry e = seq % kRingQ holds the chunk's first
+// slot (a monotone slot counter), data slots, span base and bytes. The loader
+// writes the entry, issues its DMAs and, after a counted s_waitcnt vmcnt that
+// retires them, stores ready[e] = seq + 1 (the LDS-DMA data is ordered for
+// another wave's ds_read by the issuing wave's vmcnt; the ready store comes
+// after it, and the consumer's reads come after it sees the store). A
+// consumer stores done[e] = seq + 1 once its reads of the ring have returned.
+// The loader reuses slots only behind the oldest entry not yet done (in
+// order), and before it waits for space it retires and publishes everything
+// it has issued, so no consumer can wait on a chunk held back by the loader.
+// A chunk it cannot stage (span past kRingSpanMax, descending offsets) or
+// whose frames do not all lie in their span is flagged IXG_CLS_LONG for the
+// long kernel, which runs behind this one.
+constexpr int kRingWaves = 16;
+constexpr uint32_t kRingQ = 32;
+constexpr uint32_t kRingSpanMax = 40u * 1024u;  // bytes of one chunk's span the ring stages
+constexpr uint32_t kRingInflight = 32;          // DMA instructions the loader leaves in flight at a counted wait
+constexpr int kRingAux = 0;                     // cache policy of the ring's frame loads
+// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] + [15:14]; expcnt, lgkmcnt at max)
+constexpr uint32_t vmcnt_imm(uint32_t n) { return (n & 15u) | ((n >> 4) << 14) | 0x0F70u; }
+
+struct RingQ {
+  uint32_t pos[kRingQ];    // first slot (the header) of the entry: a monotone slot counter
+  uint32_t npc[kRingQ];    // data slots after the header (0: not staged)
+  uint32_t span[kRingQ];   // bytes of the span
+  uint32_t blo[kRingQ], bhi[kRingQ];  // batch offset of the span's first byte (16-aligned)
+  uint32_t ready[kRingQ];  // seq + 1 once the entry's DMAs landed
+  uint32_t done[kRingQ];   // seq + 1 once its consumer has finished reading the ring
+  uint32_t ticket;         // consumers: the next seq to take
+};
+
+typedef __attribute__((address_space(3))) RingQ lds_ringq;
+
+DEV uint32_t lds_load(const lds_u32* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+DEV void lds_store(lds_u32* a, uint32_t v) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+
+// one 16-byte piece per lane, HBM -> LDS (dst: the wave's 1 KiB, lane l's 16 B at dst + 16 l)
+DEV void dma16(__amdgpu_buffer_rsrc_t r, lds_u32* dst, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, kRingAux);
+}
+
+// An LDS word another wave writes, read by the loader. In inline asm with its
+// own lgkmcnt wait: hipcc cannot tell an LDS read from the ring's LDS-DMA
+// destinations (no alias scopes), so for a plain read it would first wait for
+// every DMA the loader has in flight (vmcnt(0)), i.e. drain the stream.
+DEV uint32_t lds_peek(const lds_u32* a) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
+// ... and an LDS word the loader writes (for a plain store hipcc would wait for
+// every DMA in flight first: it might be one of their destinations)
+DEV void lds_poke(lds_u32* a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory"); }
+
+// The loader wave: chunks c0 .. c0 + nseq - 1 into the ring, in order. Its
+// own bookkeeping per queue entry (first slot, DMA count after the entry)
+// stays in registers (lane e holds entry e), so the loader never reads LDS
+// but the consumers' done words.
+DEV void ring_loader(const KParams& p, lds_ringq* q, lds_u32* ring, uint32_t NS, uint32_t c0, uint32_t nseq,
+                     int lane) {
+  typedef const __attribute__((address_space(4))) uint64_t c_u64;
+  typedef const __attribute__((address_space(4))) uint32_t c_u32;
+  const uint32_t n = p.n;
+  uint32_t s = 0, pos = 0, old = 0, pub = 0, issued = 0, landed = 0;
+  uint32_t vpos = 0, vend = 0;  // lane e: entry e's first slot / DMA count after it
+  auto publish = [&]() {
+    while (pub < s && (uint32_t)__builtin_amdgcn_readlane((int)vend, (int)(pub % kRingQ)) <= landed) {
+      lds_poke(&q->ready[pub % kRingQ], pub + 1u);
+      pub++;
+    }
+  };
+  // descriptors of chunk c (scalar loads): first offset, last offset and length
+  auto desc = [&](uint32_t c, uint64_t& o0, uint64_t& o1, uint32_t& l1) {
+    const uint32_t first = c * 64u, last = (first + 63u < n ? first + 63u : n - 1u);
+    o0 = *(c_u64*)(p.off + first);
+    o1 = *(c_u64*)(p.off + last);
+    const uintptr_t la = (uintptr_t)(p.len + last);
+    const uint32_t w = *(c_u32*)(la & ~(uintptr_t)3);
+    l1 = (w >> (8u * (uint32_t)(la & 2u))) & 0xffffu;
+  };
+  uint64_t o0 = 0, o1 = 0;
+  uint32_t l1 = 0;
+  if (nseq) desc(c0, o0, o1, l1);
+  while (s < nseq) {
+    const uint32_t c = c0 + s;
+    uint64_t n0 = 0, n1 = 0;
+    uint32_t nl = 0;
+    if (s + 1 < nseq) desc(c + 1, n0, n1, nl);  // the next chunk's, ahead
+    const uint64_t b16 = o0 & ~15ull, e = o1 + l1;
+    // (a batch's last chunk with a frame count that is not a multiple of 8
+    // leaves a descriptor piece half past the arrays: the long kernel takes it)
+    const uint32_t nv = n - c * 64u < 64u ? n - c * 64u : 64u;
+    const bool stage = o1 >= o0 && e > b16 && e - b16 <= kRingSpanMax && (nv & 7u) == 0u;
+    const uint32_t span = stage ? (uint32_t)(e - b16) : 0u;
+    const uint32_t npc = (span + 1023u) >> 10;
+    const uint32_t size = 1u + npc;
+    // room: at most kRingQ entries, and the slots behind the oldest entry in use
+    for (;;) {
+      while (old < s && lds_peek(&q->done[old % kRingQ]) == old + 1u) old++;
+      const uint32_t base = old < s ? (uint32_t)__builtin_amdgcn_readlane((int)vpos, (int)(old % kRingQ)) : pos;
+      if (s - old < kRingQ && pos + size - base <= NS) break;
+      // blocked: everything issued lands and is published first
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+      landed = issued;
+      publish();
+      __builtin_amdgcn_s_sleep(2);
+    }
+    const uint32_t e_ = s % kRingQ;
+    lds_poke(&q->pos[e_], pos);
+    lds_poke(&q->npc[e_], npc);
+    lds_poke(&q->span[e_], span);
+    lds_poke(&q->blo[e_], (uint32_t)b16);
+    lds_poke(&q->bhi[e_], (uint32_t)(b16 >> 32));
+    // header: the chunk's 64 offsets (512 B) and 64 lengths (128 B); rows past
+    // the batch's last frame read 0 (the descriptors' buffer extents)
+    lds_u32* hdr = ring + (pos % NS) * 256u;
+    if (lane < 32) dma16(rsrc(p.off + (uint64_t)c * 64u, 8u * nv), hdr, 16u * (uint32_t)lane);
+    if (lane < 8) dma16(rsrc(p.len + (uint64_t)c * 64u, 2u * nv), hdr + 128, 16u * (uint32_t)lane);
+    // the span, one 1 KiB slot per wave instruction (whole 16-byte pieces:
+    // the last may run up to 15 bytes into the IXG_TAIL_PAD after the batch)
+    const __amdgpu_buffer_rsrc_t rd = rsrc(p.base + b16, (span + 15u) & ~15u);
+    for (uint32_t k = 0; k < npc; k++)
+      dma16(rd, ring + ((pos + 1u + k) % NS) * 256u, 1024u * k + 16u * (uint32_t)lane);
+    issued += 2u + npc;
+    vpos = (uint32_t)lane == e_ ? pos : vpos;
+    vend = (uint32_t)lane == e_ ? issued : vend;
+    s++;
+    pos += size;
+    if (issued - landed > kRingInflight) {
+      __builtin_amdgcn_s_waitcnt(vmcnt_imm(kRingInflight));
+      landed = issued - kRingInflight;
+      publish();
+    }
+    o0 = n0;
+    o1 = n1;
+    l1 = nl;
+  }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  landed = issued;
+  publish();
+}
+
+// 4 dwords into a one's complement (end-around carry) accumulator
+DEV uint32_t adc4(uint32_t acc, const u32x4& a) {
+  asm volatile(
+      "v_add_co_u32 %0, vcc, %0, %1\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %2, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %3, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, %4, vcc\n\t"
+      "v_addc_co_u32 %0, vcc, %0, 0, vcc"
+      : "+v"(acc)
+      : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w)
+      : "vcc");
+  return acc;
+}
+
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+
+// A consumer wave: chunks by ticket until the range is done. wl / ws: the
+// wave's 64-word LDS list and tail sums.
+template <bool DMX>
+DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, lds_ringq* q, lds_u32* ring,
+                       uint32_t NS, uint32_t c0, uint32_t nseq, lds_u32* wl, lds_u32* ws, int lane) {
+  const uint32_t R = NS * 1024u;
+  bool deferred = false;
+  for (;;) {
+    uint32_t t = 0;
+    if (lane == 0) t = __hip_atomic_fetch_add(&q->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= nseq) break;
+    const uint32_t e = t % kRingQ;
+    while (lds_load(&q->ready[e]) != t + 1u) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    const uint32_t chunk = c0 + t;
+    const uint32_t pos = q->pos[e], npc = q->npc[e], span = q->span[e];
+    const uint64_t b16 = (uint64_t)q->blo[e] | ((uint64_t)q->bhi[e] << 32);
+    const lds_u32* hdr = ring + (pos % NS) * 256u;
+    const uint32_t i = chunk * 64u + (uint32_t)lane;
+    const bool valid = i < p.n;
+    const uint64_t off = (uint64_t)hdr[2 * lane] | ((uint64_t)hdr[2 * lane + 1] << 32);
+    const uint32_t L = valid ? (hdr[128 + (lane >> 1)] >> (16u * (uint32_t)(lane & 1))) & 0xffffu : 0u;
+    const uint64_t rel64 = off - b16;
+    const bool inside = !valid || L == 0u || (off >= b16 && rel64 + L <= span);
+    if (npc == 0u || !wave_all(inside)) {
+      // not staged: the long kernel behind this one takes the chunk
+      __builtin_amdgcn_s_waitcnt(kLdsWait);
+      if (lane == 0) {
+        lds_store(&q->done[e], t + 1u);
+        p.defer[chunk] = (uint8_t)IXG_CLS_LONG;
+      }
+      deferred = true;
+      continue;
+    }
+    // the frame's first byte in the ring (data slots follow the header)
+    uint32_t ra = ((pos + 1u) % NS) * 1024u + (valid ? (uint32_t)rel64 : 0u);
+    ra = ra >= R ? ra - R : ra;
+    // ---- phase R: everything read out of the ring ----
+    uint32_t d[kPrefixDw];
+    d[0] = d[1] = d[2] = 0;  // MAC addresses: never read
+    {
+      const uint32_t w0 = ra >> 2, R4 = R >> 2;
+      if (wave_all(ra + 4u * kPrefixDw <= R)) {
+        const lds_u32* f = ring + w0;
+#pragma unroll
+        for (int k = 3; k < kPrefixDw; k++) d[k] = f[k];
+      } else {
+#pragma unroll
+        for (int k = 3; k < kPrefixDw; k++) {
+          const uint32_t a = w0 + (uint32_t)k;
+          d[k] = ring[a >= R4 ? a - R4 : a];
+        }
+      }
+    }
+    // the L4 tail [96, segment end): the segment end as the parse will find
+    // it (IPv4: 14 + ip_len; IPv6 extension: 54 + payload length), summed
+    // for every frame the parse may stream (ip.c:87 / the IPv6 length check
+    // bound it by L); frames the parse does not stream ignore it
+    const uint32_t et = eth_type(d, L);
+    const bool six = (p.flags & IXG_F_IPV6) && et == 0x86DDu;
+    const uint32_t se = six ? 54u + ((byte_at(d, 18) << 8) | byte_at(d, 19)) : 14u + ((byte_at(d, 16) << 8) | byte_at(d, 17));
+    const bool cand = valid && (et == 0x0800u || six) && se > (uint32_t)kStreamBase && se <= L;
+    // ring-linear bounds (may pass R: wrapped at each read)
+    const uint32_t A = ra + (uint32_t)kStreamBase, E = ra + (cand ? se : (uint32_t)kStreamBase);
+    const uint32_t a16 = (A + 15u) & ~15u, e16 = E & ~15u;
+    auto wrap = [&](uint32_t x) { return x >= R ? x - R : x; };
+    // the owner's two partial pieces: [A, min(a16, E)) and [max(e16, a16), E)
+    uint32_t edge = 0;
+    {
+      const uint32_t hp = A & ~15u, tp = e16;
+      const u32x4 hv = *(const lds_u32x4*)(ring + (wrap(hp) >> 2));
+      const u32x4 tv = *(const lds_u32x4*)(ring + (wrap(tp) >> 2));
+      const uint32_t hh = a16 < E ? a16 : E;
+      uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, tw[4] = {tv.x, tv.y, tv.z, tv.w};
+      uint64_t es = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t xh = hp + 4u * (uint32_t)j, xt = tp + 4u * (uint32_t)j;
+        es += (xh >= A) ? keep_bytes(hw[j], (int)hh - (int)xh) : 0u;
+        es += (tp >= a16) ? keep_bytes(tw[j], (int)E - (int)xt) : 0u;
+      }
+      edge = cand ? fold32(es) : 0u;
+    }
+    // whole pieces [a16, e16) by 16-lane groups, medium segments first
+    const uint32_t npi = cand && e16 > a16 ? (e16 - a16) >> 4 : 0u;
+    const uint64_t mall = __ballot(npi != 0u), mmed = __ballot(npi != 0u && npi <= 32u);
+    const uint32_t nmed = (uint32_t)__popcll(mmed), nlist = (uint32_t)__popcll(mall);
+    if (npi) {
+      const uint64_t mine = npi <= 32u ? mmed : mall & ~mmed;
+      const uint32_t at = (npi <= 32u ? 0u : nmed) +
+                          __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
+      wl[at] = (uint32_t)lane;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t g = (uint32_t)lane >> 4, gl = (uint32_t)lane & 15u;
+    for (uint32_t k0 = 0; k0 < nlist; k0 += 4u) {
+      const uint32_t k = k0 + g;
+      const bool act = k < nlist;
+      const uint32_t owner = wl[act ? k : 0u];
+      const uint32_t oa = (uint32_t)__shfl((int)a16, (int)owner), on = act ? (uint32_t)__shfl((int)npi, (int)owner) : 0u;
+      uint32_t acc = 0;
+      for (uint32_t j = gl; wave_any(j < on); j += 16u) {
+        if (j < on) {
+          const u32x4 v = *(const lds_u32x4*)(ring + (wrap(oa + 16u * j) >> 2));
+          acc = adc4(acc, v);
+        }
+      }
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) acc = add1c(acc, (uint32_t)__shfl_xor((int)acc, m, 16));
+      if (act && gl == 0u) ws[owner] = acc;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t tail = npi ? add1c(edge, ws[lane]) : edge;
+    // every read of the ring has returned: the slots go back to the loader
+    __builtin_amdgcn_s_waitcnt(kLdsWait);
+    if (lane == 0) lds_store(&q->done[e], t + 1u);
+    // ---- phase P: parse, records ----
+    if (lane == 0) p.defer[chunk] = 0;
+    LaneState st;
+    parse_dispatch(p, tab, d, L, valid, st, t6);
+    uint32_t r4 = l4_residual(st);
+    if (st.stream) r4 = (~fold16(add1c(fold32(st.l4_acc), tail))) & 0xffffu;
+    if (valid) {
+      const Rec r = make_record(p, d, L, st, r4);
+      store_record(p, i, r, st.ip_res, r4);
+      store_demux<DMX>(p, i, r, st.src, st.dst, st.ports);
+    }
+  }
+  return deferred;
+}
+
+// LONG-mode launches of packed u64-offset batches (not mostly big chunks):
+// the ring takes every chunk. Any other launch: exits at once (block 0
+// records that in present[7], which the long kernel reads).
+extern "C" __global__ void __launch_bounds__(64 * kRingWaves) ixg_rx_ring_o(KParams p) {
+  __shared__ uint64_t T[12 * 256];
+  __shared__ RingQ q;
+  __shared__ uint32_t sh_l[kRingWaves][64], sh_s[kRingWaves][64];
+  extern __shared__ u32x4 dynr[];  // [IPv6 tables (IXG_F_IPV6)] then the ring
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool run = launch_mode(p) == IXG_MODE_LONG && !launch_big(p);
+  if (blockIdx.x == 0 && threadIdx.x == 0) p.present[7] = run ? p.epoch : 0u;
+  if (!run) return;
+  const uint32_t nchunks = (p.n + 63u) >> 6;
+  const uint32_t c0 = (uint32_t)((uint64_t)nchunks * blockIdx.x / gridDim.x);
+  const uint32_t c1 = (uint32_t)((uint64_t)nchunks * (blockIdx.x + 1) / gridDim.x);
+  const uint32_t nseq = c1 - c0;
+  const uint32_t t6w = p.tab6 ? IXG_TAB6_WORDS : 0u;
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kRingWaves)
+      dynr[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
+  lds_ringq* lq = (lds_ringq*)&q;
+  for (int k = threadIdx.x; k < (int)kRingQ; k += 64 * kRingWaves) {
+    lq->ready[k] = 0u;
+    lq->done[k] = 0u;
+  }
+  if (threadIdx.x == 0) lq->ticket = 0u;
+  stage_tables(p, T);  // (ends with the block barrier)
+  lds_u32* ring = LDS(lds_u32, dynr) + t6w;
+  const uint32_t NS = p.ring_slots;
+  bool deferred = false;
+  if (wave == 0)
+    ring_loader(p, lq, ring, NS, c0, nseq, lane);
+  else
+    deferred = ring_consumer<false>(p, Tab64{T}, LDS(const lds_u32, dynr), lq, ring, NS, c0, nseq,
+                                    LDS(lds_u32, sh_l[wave]), LDS(lds_u32, sh_s[wave]), lane);
+  if (deferred && lane == 0) p.present[IXG_CLS_LONG] = p.epoch;
+}
+
 // The sampler: one block picks the launch's IXG_MODE_*: FAST when at least
 // half of the sampled chunks could be fixed-shape by length (every frame <=
 // 64 B), else SHORT when at least half are short, else LONG.
@@ -2242,6 +2592,31 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
   const uint64_t cap = (uint64_t)ncu * (uint64_t)occupancy(k, shmem, block);
   const uint64_t g = want < cap ? want : cap;
   return g ? (uint32_t)g : 1u;
+}
+
+// The ring kernel's slots: the LDS its block leaves after its static arrays
+// and the dynamic IPv6 tables (sh6 bytes), 1 KiB each (0: cannot launch)
+static uint32_t ring_slots(size_t sh6) {
+  static std::mutex mu;
+  static int stat = -1;
+  static size_t set_for = ~(size_t)0;
+  std::lock_guard<std::mutex> lock(mu);
+  if (stat < 0) {
+    hipFuncAttributes a;
+    if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(ixg_rx_ring_o)) != hipSuccess) return 0;
+    stat = (int)a.sharedSizeBytes;
+  }
+  const size_t lds = 160u * 1024u;
+  if ((size_t)stat + sh6 + 8u * 1024u > lds) return 0;
+  const uint32_t ns = (uint32_t)((lds - (size_t)stat - sh6) / 1024u);
+  const size_t dyn = sh6 + 1024u * ns;
+  if (set_for != dyn) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(ixg_rx_ring_o), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)dyn) != hipSuccess)
+      return 0;
+    set_for = dyn;
+  }
+  return ns;
 }
 
 // The launch plan: coalesced fixed strides <= 64 B
@@ -2295,6 +2670,10 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
   // coalesced batches in the default split: the coalesced kernel finished
   // every chunk itself
   if (p.defer && coal && p.force_mode == IXG_MODE_AUTO) return (int)hipGetLastError();
+  // the ring kernel (LONG-mode launches of packed offset batches in device
+  // memory): 16-B aligned frames, offsets and lengths for its 16-byte DMAs
+  const bool ring = self && lay == 1 && !p.host_mem && ((reinterpret_cast<uintptr_t>(p.base) |
+                    reinterpret_cast<uintptr_t>(p.off) | reinterpret_cast<uintptr_t>(p.len)) & 15u) == 0u;
   if (p.defer) {
     const ShortK& ks = p.dmx ? k_short_dmx : k_short;
     // one wave per 64 chunks (frames in host memory: one per chunk)
@@ -2305,9 +2684,20 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
                        (hipStream_t)stream, ps);
   }
+  KParams pg = p;
+  if (ring) {
+    const uint32_t ns = ring_slots(sh6);
+    if (ns) {
+      pg.ring = 1u;
+      pg.ring_slots = ns;
+      const uint64_t g = nchunks < ncu ? nchunks : ncu;
+      hipLaunchKernelGGL(ixg_rx_ring_o, dim3((uint32_t)(g ? g : 1u)), dim3(64 * kRingWaves), sh6 + 1024u * ns,
+                         (hipStream_t)stream, pg);
+    }
+  }
   const kern_fn kg = k_gen[lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, p.host_mem ? wave_blocks : group_blocks, ncu, sh6)), dim3(kBlock), sh6,
-                     (hipStream_t)stream, p);
+                     (hipStream_t)stream, pg);
   return (int)hipGetLastError();
 }
 

@@ -48,7 +48,7 @@ EXPORTS = (
     "ixg_rx_hash_tables", "ixg_abi_version", "ixg_strerror", "ixg_rx_dispatch",
     "ixg_demux_load", "ixg_demux_batch_dev", "ixg_demux_batch_host", "ixg_rx_demux_batch_dev",
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
-    "ixg_ev_batch_dev", "ixg_rx_set_split", "ixg_rx_set_fdir",
+    "ixg_ev_batch_dev", "ixg_rx_set_split", "ixg_rx_set_fdir", "ixg_rx_launch_info",
     "ixg_rx_async_init", "ixg_rx_submit_mbufs", "ixg_rx_flush", "ixg_rx_poll", "ixg_rx_async_pending",
     "ixg_rx_register_memory", "ixg_rx_unregister_memory", "ixg_tcp_ext_batch_dev",
 )
@@ -143,6 +143,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_dispatch.restype = u32
     lib.ixg_rx_set_split.argtypes = [vp, u32]
     lib.ixg_rx_set_split.restype = i32
+    lib.ixg_rx_launch_info.argtypes = [vp, vp]
+    lib.ixg_rx_launch_info.restype = i32
     lib.ixg_rx_set_fdir.argtypes = [vp, vp, u32, ctypes.c_uint16]
     lib.ixg_rx_set_fdir.restype = i32
     lib.ixg_rx_async_init.argtypes = [vp, ctypes.POINTER(AsyncCfg)]
@@ -201,6 +203,13 @@ class RxEngine:
 
     def set_split(self, split: str) -> None:
         _check(self._lib.ixg_rx_set_split(self._ctx, SPLITS[split]), "ixg_rx_set_split", self._lib)
+
+    def launch_info(self) -> dict:
+        """The last launch's split as the device chose it (ixg_rx_launch_info)."""
+        info = np.zeros(3, dtype=np.uint32)
+        _check(self._lib.ixg_rx_launch_info(self._ctx, info.ctypes.data), "ixg_rx_launch_info", self._lib)
+        modes = {0: "fast", 1: "short", 2: "long"}
+        return {"mode": modes.get(int(info[0])), "ring": bool(info[1]), "big": bool(info[2])}
 
     def set_fdir(self, filters, cpu_id: int = 0) -> None:
         """Flow-director perfect filters (FDIR_DTYPE array; empty = none)."""
