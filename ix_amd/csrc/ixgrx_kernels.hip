@@ -2237,17 +2237,22 @@ constexpr int kRingWaves = 16;
 constexpr uint32_t kRingQ = 32;
 constexpr uint32_t kRingSpanMax = 40u * 1024u;  // bytes of one chunk's span the ring stages
 constexpr uint32_t kRingInflight = 32;          // DMA instructions the loader leaves in flight at a counted wait
+constexpr uint32_t kRingQD = 16;                // header queue slots (a chunk's descriptor rows)
+constexpr uint32_t kRingHdr = 640;              // bytes per header slot: 64 u64 offsets + 64 u16 lengths
+constexpr uint32_t kRingHA = 8;                 // headers issued this many chunks ahead of the data
 constexpr int kRingAux = 0;                     // cache policy of the ring's frame loads
 // s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] + [15:14]; expcnt, lgkmcnt at max)
 constexpr uint32_t vmcnt_imm(uint32_t n) { return (n & 15u) | ((n >> 4) << 14) | 0x0F70u; }
 
+constexpr int kRingLoaders = 2;                 // loader waves (waves 0 .. kRingLoaders-1)
 struct RingQ {
-  uint32_t pos[kRingQ];    // first slot (the header) of the entry: a monotone slot counter
-  uint32_t npc[kRingQ];    // data slots after the header (0: not staged)
+  uint32_t pos[kRingQ];    // first data slot of the entry: a monotone slot counter
+  uint32_t npc[kRingQ];    // data slots (0: not staged)
   uint32_t span[kRingQ];   // bytes of the span
   uint32_t blo[kRingQ], bhi[kRingQ];  // batch offset of the span's first byte (16-aligned)
-  uint32_t ready[kRingQ];  // seq + 1 once the entry's DMAs landed
+  uint32_t ready[kRingLoaders][kRingQ];  // seq + 1 once the loader's share of the entry's DMAs landed
   uint32_t done[kRingQ];   // seq + 1 once its consumer has finished reading the ring
+  uint32_t hready[kRingQD];  // seq + 1 once the chunk's header landed (loader 0 publishes it)
   uint32_t ticket;         // consumers: the next seq to take
 };
 
@@ -2274,88 +2279,142 @@ DEV uint32_t lds_peek(const lds_u32* a) {
 // every DMA in flight first: it might be one of their destinations)
 DEV void lds_poke(lds_u32* a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory"); }
 
-// The loader wave: chunks c0 .. c0 + nseq - 1 into the ring, in order. Its
-// own bookkeeping per queue entry (first slot, DMA count after the entry)
-// stays in registers (lane e holds entry e), so the loader never reads LDS
-// but the consumers' done words.
-DEV void ring_loader(const KParams& p, lds_ringq* q, lds_u32* ring, uint32_t NS, uint32_t c0, uint32_t nseq,
-                     int lane) {
-  typedef const __attribute__((address_space(4))) uint64_t c_u64;
-  typedef const __attribute__((address_space(4))) uint32_t c_u32;
+// s_waitcnt vmcnt(n) with n an immediate: the largest rung of the ladder
+// that is <= k (every DMA older than the k youngest has then landed).
+// Returns the rung waited for.
+DEV uint32_t vm_ladder(uint32_t k) {
+  if (k >= 48u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(48)); return 48u; }
+  if (k >= 32u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(32)); return 32u; }
+  if (k >= 16u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(16)); return 16u; }
+  if (k >= 8u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(8)); return 8u; }
+  if (k >= 4u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(4)); return 4u; }
+  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
+  return 0u;
+}
+
+// The loader waves: chunks c0 .. c0 + nseq - 1 into the ring, in order. Each
+// of the kRingLoaders waves runs the same walk and issues its share of every
+// chunk's 1 KiB pieces (piece k: loader k mod kRingLoaders); one loader wave
+// alone tops out near 25 GB/s per CU (MI355X_MICROARCH.md ldsdma-fill), which
+// is C3's whole per-CU rate. Loader 0 also keeps every chunk's descriptor
+// rows (64 offsets + 64 lengths, 640 B) kRingHA chunks ahead in a header
+// queue of kRingQD slots and publishes each header once landed; the chunk's
+// span is read from it, so no loader has a load of its own to wait for (a
+// scalar load's lgkmcnt(0) also waits for whatever else is in flight on that
+// counter). Bookkeeping per queue entry stays in registers (lane e holds
+// entry e): first slot, DMA count after the header, after the loader's
+// share of the data. A loader waits on a DMA only when it needs it: the
+// header it is about to read, or, when the ring is full, the oldest chunk
+// it has not yet published.
+DEV void ring_loader(const KParams& p, lds_ringq* q, lds_u32* hq, lds_u32* ring, uint32_t NS, uint32_t c0,
+                     uint32_t nseq, int lane, uint32_t li) {
   const uint32_t n = p.n;
-  uint32_t s = 0, pos = 0, old = 0, pub = 0, issued = 0, landed = 0;
-  uint32_t vpos = 0, vend = 0;  // lane e: entry e's first slot / DMA count after it
+  uint32_t s = 0, hs = 0, pos = 0, wpos = 0, old = 0, pub = 0, issued = 0, landed = 0;
+  uint32_t vpos = 0, vhdr = 0, vend = 0;
+  auto rl = [](uint32_t v, uint32_t e) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(e % kRingQ)); };
   auto publish = [&]() {
-    while (pub < s && (uint32_t)__builtin_amdgcn_readlane((int)vend, (int)(pub % kRingQ)) <= landed) {
-      lds_poke(&q->ready[pub % kRingQ], pub + 1u);
+    while (pub < s && rl(vend, pub) <= landed) {
+      lds_poke(&q->ready[li][pub % kRingQ], pub + 1u);
       pub++;
     }
   };
-  // descriptors of chunk c (scalar loads): first offset, last offset and length
-  auto desc = [&](uint32_t c, uint64_t& o0, uint64_t& o1, uint32_t& l1) {
-    const uint32_t first = c * 64u, last = (first + 63u < n ? first + 63u : n - 1u);
-    o0 = *(c_u64*)(p.off + first);
-    o1 = *(c_u64*)(p.off + last);
-    const uintptr_t la = (uintptr_t)(p.len + last);
-    const uint32_t w = *(c_u32*)(la & ~(uintptr_t)3);
-    l1 = (w >> (8u * (uint32_t)(la & 2u))) & 0xffffu;
+  auto wait_for = [&](uint32_t idx) {  // the DMA that brought the count to idx has landed
+    if (landed >= idx) return;
+    landed = issued - vm_ladder(issued - idx);
+    publish();
   };
-  uint64_t o0 = 0, o1 = 0;
-  uint32_t l1 = 0;
-  if (nseq) desc(c0, o0, o1, l1);
+  auto headers = [&]() {
+    while (li == 0u && hs < nseq && hs < s + kRingHA && hs - old < kRingQD) {
+      const uint32_t c = c0 + hs;
+      const uint32_t nv = n - c * 64u < 64u ? n - c * 64u : 64u;
+      lds_u32* h = hq + (hs % kRingQD) * (kRingHdr / 4u);
+      if (lane < 32) dma16(rsrc(p.off + (uint64_t)c * 64u, 8u * nv), h, 16u * (uint32_t)lane);
+      if (lane < 8) dma16(rsrc(p.len + (uint64_t)c * 64u, 2u * nv), h + 128, 16u * (uint32_t)lane);
+      issued += 2u;
+      vhdr = (uint32_t)lane == hs % kRingQ ? issued : vhdr;
+      hs++;
+    }
+  };
+  auto advance = [&]() {
+    while (old < s && lds_peek(&q->done[old % kRingQ]) == old + 1u) old++;
+  };
+  // nothing to issue yet: publish what has landed, oldest first (consumers
+  // free the ring only behind chunks every loader published), else sleep
+  auto idle = [&]() {
+    if (pub < s) {
+      wait_for(rl(vend, pub));
+    } else {
+      headers();
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
   while (s < nseq) {
+    headers();
+    if (li == 0u) {
+      wait_for(rl(vhdr, s));
+      lds_poke(&q->hready[s % kRingQD], s + 1u);
+    } else {
+      while (lds_peek(&q->hready[s % kRingQD]) != s + 1u) idle();
+    }
     const uint32_t c = c0 + s;
-    uint64_t n0 = 0, n1 = 0;
-    uint32_t nl = 0;
-    if (s + 1 < nseq) desc(c + 1, n0, n1, nl);  // the next chunk's, ahead
+    const uint32_t nv = n - c * 64u < 64u ? n - c * 64u : 64u;
+    const lds_u32* h = hq + (s % kRingQD) * (kRingHdr / 4u);
+    // the first offset, the last offset and the last length, one LDS round trip
+    uint64_t o0, o1;
+    uint32_t lw;
+    asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&v"(o0), "=&v"(o1), "=&v"(lw)
+                 : "v"(h), "v"(h + 2u * (nv - 1u)), "v"(h + 128u + ((nv - 1u) >> 1))
+                 : "memory");
+    o0 = rfl64(o0);
+    o1 = rfl64(o1);
+    const uint32_t l1 = (__builtin_amdgcn_readfirstlane(lw) >> (16u * ((nv - 1u) & 1u))) & 0xffffu;
     const uint64_t b16 = o0 & ~15ull, e = o1 + l1;
     // (a batch's last chunk with a frame count that is not a multiple of 8
-    // leaves a descriptor piece half past the arrays: the long kernel takes it)
-    const uint32_t nv = n - c * 64u < 64u ? n - c * 64u : 64u;
+    // has a descriptor piece half past the arrays: the long kernel takes it)
     const bool stage = o1 >= o0 && e > b16 && e - b16 <= kRingSpanMax && (nv & 7u) == 0u;
     const uint32_t span = stage ? (uint32_t)(e - b16) : 0u;
     const uint32_t npc = (span + 1023u) >> 10;
-    const uint32_t size = 1u + npc;
     // room: at most kRingQ entries, and the slots behind the oldest entry in use
     for (;;) {
-      while (old < s && lds_peek(&q->done[old % kRingQ]) == old + 1u) old++;
-      const uint32_t base = old < s ? (uint32_t)__builtin_amdgcn_readlane((int)vpos, (int)(old % kRingQ)) : pos;
-      if (s - old < kRingQ && pos + size - base <= NS) break;
-      // blocked: everything issued lands and is published first
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-      landed = issued;
-      publish();
-      __builtin_amdgcn_s_sleep(2);
+      advance();
+      const uint32_t base = old < s ? rl(vpos, old) : pos;
+      if (s - old < kRingQ && pos + npc - base <= NS) break;
+      idle();
     }
     const uint32_t e_ = s % kRingQ;
-    lds_poke(&q->pos[e_], pos);
-    lds_poke(&q->npc[e_], npc);
-    lds_poke(&q->span[e_], span);
-    lds_poke(&q->blo[e_], (uint32_t)b16);
-    lds_poke(&q->bhi[e_], (uint32_t)(b16 >> 32));
-    // header: the chunk's 64 offsets (512 B) and 64 lengths (128 B); rows past
-    // the batch's last frame read 0 (the descriptors' buffer extents)
-    lds_u32* hdr = ring + (pos % NS) * 256u;
-    if (lane < 32) dma16(rsrc(p.off + (uint64_t)c * 64u, 8u * nv), hdr, 16u * (uint32_t)lane);
-    if (lane < 8) dma16(rsrc(p.len + (uint64_t)c * 64u, 2u * nv), hdr + 128, 16u * (uint32_t)lane);
-    // the span, one 1 KiB slot per wave instruction (whole 16-byte pieces:
-    // the last may run up to 15 bytes into the IXG_TAIL_PAD after the batch)
+    if (li == 0u) {
+      lds_poke(&q->pos[e_], pos);
+      lds_poke(&q->npc[e_], npc);
+      lds_poke(&q->span[e_], span);
+      lds_poke(&q->blo[e_], (uint32_t)b16);
+      lds_poke(&q->bhi[e_], (uint32_t)(b16 >> 32));
+    }
+    // this loader's pieces of the span, one 1 KiB slot per wave instruction
+    // (whole 16-byte pieces: the last may run up to 15 bytes into the
+    // IXG_TAIL_PAD after the batch)
     const __amdgpu_buffer_rsrc_t rd = rsrc(p.base + b16, (span + 15u) & ~15u);
-    for (uint32_t k = 0; k < npc; k++)
-      dma16(rd, ring + ((pos + 1u + k) % NS) * 256u, 1024u * k + 16u * (uint32_t)lane);
-    issued += 2u + npc;
+    uint32_t slot = wpos + li;
+    slot = slot >= NS ? slot - NS : slot;
+    uint32_t mine = 0;
+    for (uint32_t k = li; k < npc; k += kRingLoaders) {
+      dma16(rd, ring + slot * 256u, 1024u * k + 16u * (uint32_t)lane);
+      slot += kRingLoaders;
+      slot = slot >= NS ? slot - NS : slot;
+      mine++;
+    }
+    issued += mine;
     vpos = (uint32_t)lane == e_ ? pos : vpos;
     vend = (uint32_t)lane == e_ ? issued : vend;
     s++;
-    pos += size;
+    pos += npc;
+    wpos += npc;
+    wpos = wpos >= NS ? wpos - NS : wpos;
     if (issued - landed > kRingInflight) {
       __builtin_amdgcn_s_waitcnt(vmcnt_imm(kRingInflight));
       landed = issued - kRingInflight;
       publish();
     }
-    o0 = n0;
-    o1 = n1;
-    l1 = nl;
   }
   __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
   landed = issued;
@@ -2378,12 +2437,21 @@ DEV uint32_t adc4(uint32_t acc, const u32x4& a) {
 
 typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 
+// DPP lane moves within rows of 16 (no LDS round trip, unlike ds_bpermute)
+template <int CTRL>
+DEV uint32_t dpp(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
+}
+constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
 // A consumer wave: chunks by ticket until the range is done. wl / ws: the
 // wave's 64-word LDS list and tail sums.
 template <bool DMX>
-DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, lds_ringq* q, lds_u32* ring,
-                       uint32_t NS, uint32_t c0, uint32_t nseq, lds_u32* wl, lds_u32* ws, int lane) {
+DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, lds_ringq* q, const lds_u32* hq,
+                       const lds_u32* ring, uint32_t NS, uint32_t c0, uint32_t nseq, lds_u32* wl, lds_u32* ws,
+                       int lane) {
   const uint32_t R = NS * 1024u;
+  auto wrap = [&](uint32_t x) { return x >= R ? x - R : x; };
   bool deferred = false;
   for (;;) {
     uint32_t t = 0;
@@ -2391,12 +2459,13 @@ DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, ld
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= nseq) break;
     const uint32_t e = t % kRingQ;
-    while (lds_load(&q->ready[e]) != t + 1u) __builtin_amdgcn_s_sleep(1);
+    for (int l = 0; l < kRingLoaders; l++)
+      while (lds_load(&q->ready[l][e]) != t + 1u) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
     const uint32_t chunk = c0 + t;
     const uint32_t pos = q->pos[e], npc = q->npc[e], span = q->span[e];
     const uint64_t b16 = (uint64_t)q->blo[e] | ((uint64_t)q->bhi[e] << 32);
-    const lds_u32* hdr = ring + (pos % NS) * 256u;
+    const lds_u32* hdr = hq + (t % kRingQD) * (kRingHdr / 4u);
     const uint32_t i = chunk * 64u + (uint32_t)lane;
     const bool valid = i < p.n;
     const uint64_t off = (uint64_t)hdr[2 * lane] | ((uint64_t)hdr[2 * lane + 1] << 32);
@@ -2413,9 +2482,8 @@ DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, ld
       deferred = true;
       continue;
     }
-    // the frame's first byte in the ring (data slots follow the header)
-    uint32_t ra = ((pos + 1u) % NS) * 1024u + (valid ? (uint32_t)rel64 : 0u);
-    ra = ra >= R ? ra - R : ra;
+    // the frame's first byte in the ring
+    const uint32_t ra = wrap((pos % NS) * 1024u + (valid ? (uint32_t)rel64 : 0u));
     // ---- phase R: everything read out of the ring ----
     uint32_t d[kPrefixDw];
     d[0] = d[1] = d[2] = 0;  // MAC addresses: never read
@@ -2444,7 +2512,6 @@ DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, ld
     // ring-linear bounds (may pass R: wrapped at each read)
     const uint32_t A = ra + (uint32_t)kStreamBase, E = ra + (cand ? se : (uint32_t)kStreamBase);
     const uint32_t a16 = (A + 15u) & ~15u, e16 = E & ~15u;
-    auto wrap = [&](uint32_t x) { return x >= R ? x - R : x; };
     // the owner's two partial pieces: [A, min(a16, E)) and [max(e16, a16), E)
     uint32_t edge = 0;
     {
@@ -2462,32 +2529,54 @@ DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, ld
       }
       edge = cand ? fold32(es) : 0u;
     }
-    // whole pieces [a16, e16) by 16-lane groups, medium segments first
+    // whole pieces [a16, e16): medium segments (<= 32 pieces) by 4-lane
+    // groups, longer ones by 16-lane groups, packed over the wave's lanes
+    // (medium entries first, long ones from a 16-aligned lane on), 64 lanes
+    // per round; every lane issues its (up to 8) piece reads at once, then
+    // sums them, then the group folds its lanes together by DPP
     const uint32_t npi = cand && e16 > a16 ? (e16 - a16) >> 4 : 0u;
-    const uint64_t mall = __ballot(npi != 0u), mmed = __ballot(npi != 0u && npi <= 32u);
-    const uint32_t nmed = (uint32_t)__popcll(mmed), nlist = (uint32_t)__popcll(mall);
+    const bool med = npi != 0u && npi <= 32u;
+    const uint64_t mmed = __ballot(med), mlng = __ballot(npi > 32u);
+    const uint32_t nmed = (uint32_t)__popcll(mmed), nlng = (uint32_t)__popcll(mlng);
     if (npi) {
-      const uint64_t mine = npi <= 32u ? mmed : mall & ~mmed;
-      const uint32_t at = (npi <= 32u ? 0u : nmed) +
+      // the entry: {owner lane | pieces << 8, first piece's ring address}
+      const uint64_t mine = med ? mmed : mlng;
+      const uint32_t at = (med ? 0u : nmed) +
                           __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
-      wl[at] = (uint32_t)lane;
+      typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+      *(__attribute__((address_space(3))) u32x2v*)(wl + 2u * at) = u32x2v{(uint32_t)lane | (npi << 8), a16};
     }
     __builtin_amdgcn_wave_barrier();
-    const uint32_t g = (uint32_t)lane >> 4, gl = (uint32_t)lane & 15u;
-    for (uint32_t k0 = 0; k0 < nlist; k0 += 4u) {
-      const uint32_t k = k0 + g;
-      const bool act = k < nlist;
-      const uint32_t owner = wl[act ? k : 0u];
-      const uint32_t oa = (uint32_t)__shfl((int)a16, (int)owner), on = act ? (uint32_t)__shfl((int)npi, (int)owner) : 0u;
+    const uint32_t lstart = (4u * nmed + 15u) & ~15u, total = lstart + 16u * nlng;
+    for (uint32_t v0 = 0; v0 < total; v0 += 64u) {
+      const uint32_t v = v0 + (uint32_t)lane;
+      const bool big = v >= lstart;
+      const uint32_t G = big ? 16u : 4u;
+      const uint32_t k = big ? nmed + ((v - lstart) >> 4) : v >> 2;
+      const bool act = big ? v < total : k < nmed;
+      const uint32_t gl = v & (G - 1u);
+      typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+      const u32x2v ent = *(const __attribute__((address_space(3))) u32x2v*)(wl + 2u * (act ? k : 0u));
+      const uint32_t owner = ent.x & 63u, oa = ent.y, on = act ? ent.x >> 8 : 0u;
       uint32_t acc = 0;
-      for (uint32_t j = gl; wave_any(j < on); j += 16u) {
-        if (j < on) {
-          const u32x4 v = *(const lds_u32x4*)(ring + (wrap(oa + 16u * j) >> 2));
-          acc = adc4(acc, v);
+      for (uint32_t j0 = gl; wave_any(j0 < on); j0 += 8u * G) {
+        u32x4 pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t j = j0 + G * (uint32_t)u;
+          pv[u] = *(const lds_u32x4*)(ring + (wrap(oa + 16u * (j < on ? j : 0u)) >> 2));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const uint32_t m = 0u - (uint32_t)(j0 + G * (uint32_t)u < on);
+          acc = adc4(acc, u32x4{pv[u].x & m, pv[u].y & m, pv[u].z & m, pv[u].w & m});
         }
       }
-#pragma unroll
-      for (int m = 1; m < 16; m <<= 1) acc = add1c(acc, (uint32_t)__shfl_xor((int)acc, m, 16));
+      acc = add1c(acc, dpp<kDppQuadXor1>(acc));
+      acc = add1c(acc, dpp<kDppQuadXor2>(acc));
+      const uint32_t s8 = add1c(acc, dpp<kDppHalfMirror>(acc));
+      const uint32_t s16 = add1c(s8, dpp<kDppMirror>(s8));
+      acc = big ? s16 : acc;
       if (act && gl == 0u) ws[owner] = acc;
     }
     __builtin_amdgcn_wave_barrier();
@@ -2516,7 +2605,7 @@ DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, ld
 extern "C" __global__ void __launch_bounds__(64 * kRingWaves) ixg_rx_ring_o(KParams p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ RingQ q;
-  __shared__ uint32_t sh_l[kRingWaves][64], sh_s[kRingWaves][64];
+  __shared__ uint32_t sh_l[kRingWaves][128], sh_s[kRingWaves][64];
   extern __shared__ u32x4 dynr[];  // [IPv6 tables (IXG_F_IPV6)] then the ring
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool run = launch_mode(p) == IXG_MODE_LONG && !launch_big(p);
@@ -2533,18 +2622,20 @@ extern "C" __global__ void __launch_bounds__(64 * kRingWaves) ixg_rx_ring_o(KPar
   }
   lds_ringq* lq = (lds_ringq*)&q;
   for (int k = threadIdx.x; k < (int)kRingQ; k += 64 * kRingWaves) {
-    lq->ready[k] = 0u;
+    for (int l = 0; l < kRingLoaders; l++) lq->ready[l][k] = 0u;
     lq->done[k] = 0u;
+    if (k < (int)kRingQD) lq->hready[k] = 0u;
   }
   if (threadIdx.x == 0) lq->ticket = 0u;
   stage_tables(p, T);  // (ends with the block barrier)
-  lds_u32* ring = LDS(lds_u32, dynr) + t6w;
+  lds_u32* hq = LDS(lds_u32, dynr) + t6w;
+  lds_u32* ring = hq + kRingQD * kRingHdr / 4u;
   const uint32_t NS = p.ring_slots;
   bool deferred = false;
-  if (wave == 0)
-    ring_loader(p, lq, ring, NS, c0, nseq, lane);
+  if (wave < kRingLoaders)
+    ring_loader(p, lq, hq, ring, NS, c0, nseq, lane, (uint32_t)wave);
   else
-    deferred = ring_consumer<false>(p, Tab64{T}, LDS(const lds_u32, dynr), lq, ring, NS, c0, nseq,
+    deferred = ring_consumer<false>(p, Tab64{T}, LDS(const lds_u32, dynr), lq, hq, ring, NS, c0, nseq,
                                     LDS(lds_u32, sh_l[wave]), LDS(lds_u32, sh_s[wave]), lane);
   if (deferred && lane == 0) p.present[IXG_CLS_LONG] = p.epoch;
 }
@@ -2606,10 +2697,10 @@ static uint32_t ring_slots(size_t sh6) {
     if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(ixg_rx_ring_o)) != hipSuccess) return 0;
     stat = (int)a.sharedSizeBytes;
   }
-  const size_t lds = 160u * 1024u;
-  if ((size_t)stat + sh6 + 8u * 1024u > lds) return 0;
-  const uint32_t ns = (uint32_t)((lds - (size_t)stat - sh6) / 1024u);
-  const size_t dyn = sh6 + 1024u * ns;
+  const size_t lds = 160u * 1024u, hq = (size_t)kRingQD * kRingHdr;
+  if ((size_t)stat + sh6 + hq + 48u * 1024u > lds) return 0;
+  const uint32_t ns = (uint32_t)((lds - (size_t)stat - sh6 - hq) / 1024u);
+  const size_t dyn = sh6 + hq + 1024u * ns;
   if (set_for != dyn) {
     if (hipFuncSetAttribute(reinterpret_cast<const void*>(ixg_rx_ring_o), hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)dyn) != hipSuccess)
@@ -2691,7 +2782,8 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
       pg.ring = 1u;
       pg.ring_slots = ns;
       const uint64_t g = nchunks < ncu ? nchunks : ncu;
-      hipLaunchKernelGGL(ixg_rx_ring_o, dim3((uint32_t)(g ? g : 1u)), dim3(64 * kRingWaves), sh6 + 1024u * ns,
+      hipLaunchKernelGGL(ixg_rx_ring_o, dim3((uint32_t)(g ? g : 1u)), dim3(64 * kRingWaves),
+                         sh6 + (size_t)kRingQD * kRingHdr + 1024u * ns,
                          (hipStream_t)stream, pg);
     }
   }

@@ -14,7 +14,7 @@
 #   sq:W+W+...       SQ counter passes per workload (tools/sq_counters.sh)
 #   mem:W+W+...      memory-pipe counter pass per workload (tools/mem_counters.sh)
 #   profile          the round profile: kernel trace of the default bench, PMC traffic (tools/profile_round.sh)
-#   ab:A,B,...       same-process A/B of kernel variants (tools/ab_fast.py A B ...)
+#   ab:W:L1,L2,...   same-process A/B of library builds over workload W (tools/ab_lib.py; tools/build_variant.sh)
 #   py:SCRIPT,A,...  python3 SCRIPT A ... (a probe or a one-off measurement) -> py_<i>.log
 set -o pipefail
 TAG=${1:?tag}; shift
@@ -48,7 +48,7 @@ for STEP in "$@"; do
     sq) timeout -k 10 900 bash tools/sq_counters.sh "$TAG/sq_$i" "${args//+/ }" ;;
     mem) timeout -k 10 600 bash tools/mem_counters.sh "$TAG/mem_$i" "${args//+/ }" ;;
     profile) timeout -k 10 1000 bash tools/profile_round.sh "$TAG/profile" ;;
-    ab) timeout -k 10 900 python3 -u tools/ab_fast.py $args > "$O/ab_$i.json" 2> "$O/ab_$i.log" ;;
+    ab) timeout -k 10 900 python3 -u tools/ab_lib.py --workload "${arg%%:*}" --libs "${arg#*:}" > "$O/ab_$i.json" 2> "$O/ab_$i.log" ;;
     py) timeout -k 10 600 python3 -u $args > "$O/py_$i.log" 2>&1 ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
