@@ -30,6 +30,7 @@
  */
 #define _GNU_SOURCE
 #include <pthread.h>
+#include <sys/resource.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -160,6 +161,12 @@ struct worker {
 	size_t nlat, cap_lat;
 	struct ixg_rx_rec *dump;
 	uint32_t ndump;
+	/* where the thread's time went: the library's counters, the callees, the
+	 * longest gap between two passes of the loop (the thread not running,
+	 * or stuck in a call), the scheduler's context switches */
+	struct ixg_rx_async_stats ast;
+	double t_dispatch, max_gap;
+	long nvcsw, nivcsw;
 };
 
 static pthread_barrier_t bar;
@@ -189,8 +196,15 @@ static void *work(void *arg)
 	const uint32_t n = opt.arena;
 	uint64_t sub = 0, got = 0; /* frames submitted / polled */
 	uint32_t pos = 0;
+	ixg_rx_async_stats(w->ctx, NULL, 1);
+	struct rusage ru0;
+	getrusage(RUSAGE_THREAD, &ru0);
+	double t_prev = now_s();
 	for (;;) {
 		const double t = now_s();
+		if (t - t_prev > w->max_gap)
+			w->max_gap = t - t_prev;
+		t_prev = t;
 		const int more = t < w->t_end;
 		if (more) {
 			/* one sys_bpoll iteration: up to `batch` frames off the RX queue */
@@ -221,7 +235,9 @@ static void *work(void *arg)
 			break;
 		}
 		if (r > 0) {
+			const double d0 = now_s();
 			ixg_rx_dispatch(pm, pr, (uint32_t)r, &ops, &w->st);
+			w->t_dispatch += now_s() - d0;
 			if (w->dump && w->ndump < pool_n) {
 				uint32_t c = (uint32_t)r < pool_n - w->ndump ? (uint32_t)r : pool_n - w->ndump;
 				memcpy(w->dump + w->ndump, pr, c * sizeof(*pr));
@@ -237,6 +253,11 @@ static void *work(void *arg)
 		}
 	}
 	w->frames_done = got;
+	ixg_rx_async_stats(w->ctx, &w->ast, 0);
+	struct rusage ru1;
+	getrusage(RUSAGE_THREAD, &ru1);
+	w->nvcsw = ru1.ru_nvcsw - ru0.ru_nvcsw;
+	w->nivcsw = ru1.ru_nivcsw - ru0.ru_nivcsw;
 	free(pm);
 	free(pr);
 	free(q_seq);
@@ -303,6 +324,28 @@ static int run_loop(void)
 		st.drop += ws[i].st.drop;
 		nl += ws[i].nlat;
 	}
+	/* the per-thread breakdown, summed over threads (ns per frame of each
+	 * part of a thread's time; the rest is the loop itself and waiting) */
+	double g_ns = 0, l_ns = 0, p_ns = 0, w_ns = 0, d_s = 0, gap = 0;
+	uint64_t batches = 0, by_time = 0, refused = 0, offered = 0;
+	long vcs = 0, ivcs = 0;
+	for (int i = 0; i < opt.threads; i++) {
+		const struct ixg_rx_async_stats *a = &ws[i].ast;
+		g_ns += (double)a->gather_ns;
+		l_ns += (double)a->launch_ns;
+		p_ns += (double)a->poll_ns;
+		w_ns += (double)a->wait_ns;
+		d_s += ws[i].t_dispatch;
+		batches += a->batches;
+		by_time += a->batches_by_time;
+		refused += a->frames_refused;
+		offered += a->frames_refused + a->frames_submitted;
+		vcs += ws[i].nvcsw;
+		ivcs += ws[i].nivcsw;
+		if (ws[i].max_gap > gap)
+			gap = ws[i].max_gap;
+	}
+	const double fr = frames ? (double)frames : 1.0;
 	double *lat = malloc((nl ? nl : 1) * sizeof(double));
 	size_t o = 0;
 	for (int i = 0; i < opt.threads; i++) {
@@ -327,13 +370,20 @@ static int run_loop(void)
 	       "\"staged_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
 	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d, "
 	       "\"zero_copy\": %d}, "
-	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}}\n",
+	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}, "
+	       "\"breakdown\": {\"thread_ns_per_frame\": %.2f, \"gather_ns_per_frame\": %.2f, \"launch_us_per_batch\": %.2f, "
+	       "\"poll_ns_per_frame\": %.2f, \"wait_ns_per_frame\": %.2f, \"dispatch_ns_per_frame\": %.2f, "
+	       "\"frames_per_batch\": %.0f, \"batches_by_time\": %.3f, \"refused_share\": %.3f, "
+	       "\"max_loop_gap_us\": %.1f, \"context_switches\": {\"voluntary\": %ld, \"involuntary\": %ld}}}\n",
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
 	       nl ? lat[nl - 1] : 0.0, nl, staged_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
 	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, (unsigned long long)st.tcp,
 	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
-	       (unsigned long long)st.drop);
+	       (unsigned long long)st.drop, el * opt.threads * 1e9 / fr, g_ns / fr,
+	       batches ? l_ns / (double)batches / 1e3 : 0.0, p_ns / fr, w_ns / fr, d_s * 1e9 / fr,
+	       batches ? fr / (double)batches : 0.0, batches ? (double)by_time / (double)batches : 0.0,
+	       offered ? (double)refused / (double)offered : 0.0, gap * 1e6, vcs, ivcs);
 	if (opt.dump) {
 		FILE *f = fopen(opt.dump, "wb");
 		if (!f || fwrite(ws[0].dump, sizeof(struct ixg_rx_rec), ws[0].ndump, f) != ws[0].ndump)

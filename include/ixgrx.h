@@ -232,6 +232,25 @@ int ixg_rx_poll(void *ctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max, 
 /* Frames submitted and not yet returned by poll, or -errno. */
 int ixg_rx_async_pending(void *ctx);
 
+/* Where a context's asynchronous path spends its host time (cumulative since
+ * ixg_rx_async_init or the last reset; for tuning IX's loop, e.g. the thread
+ * count or the batch size). Times are host nanoseconds measured with the TSC
+ * inside the calls. */
+struct ixg_rx_async_stats {
+	uint64_t frames_submitted; /* accepted by submit */
+	uint64_t frames_returned;  /* handed back by poll */
+	uint64_t frames_refused;   /* offered to submit, not accepted (every batch busy) */
+	uint64_t submit_calls, poll_calls;
+	uint64_t batches;          /* launched */
+	uint64_t batches_by_time;  /* ... of which before they were full (max_wait_us passed, flush, poll with wait) */
+	uint64_t gather_ns;        /* submit: copying frames into the pinned staging */
+	uint64_t launch_ns;        /* enqueuing batches: copies, kernels, event */
+	uint64_t poll_ns;          /* poll: event queries and copying records out */
+	uint64_t wait_ns;          /* poll with wait != 0: blocked on the GPU */
+};
+/* Copy the counters to *out (may be NULL) and, reset != 0, zero them. 0 or -errno. */
+int ixg_rx_async_stats(void *ctx, struct ixg_rx_async_stats *out, int reset);
+
 /* Zero copy: make host memory that holds mbufs (IX's mbuf mempool, its 2 MB
  * pages, dp/core/mempool.c:198-243) readable by the kernels (page-locked and
  * mapped, hipHostRegister). With IXG_ASYNC_DIRECT, a submitted frame whose

@@ -45,6 +45,8 @@ struct ixg_abatch {
 
 struct ixg_async {
 	struct ixg_rx_async_cfg cfg;
+	struct ixg_rx_async_stats st; /* the *_ns fields in TSC ticks until read */
+	uint64_t tsc0, ns0;           /* calibration: a TSC reading and the clock with it */
 	uint32_t head;       /* oldest batch not yet fully polled */
 	uint32_t tail;       /* next batch to open */
 	uint32_t count;      /* batches in the ring that are not FREE */
@@ -60,6 +62,17 @@ static uint64_t now_ns(void)
 	struct timespec t;
 	clock_gettime(CLOCK_MONOTONIC, &t);
 	return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+
+/* the stats' clock: the TSC (a few ns per reading; converted to ns against
+ * CLOCK_MONOTONIC over the context's lifetime when the stats are read) */
+static inline uint64_t tsc(void)
+{
+#if defined(__x86_64__)
+	return __builtin_ia32_rdtsc();
+#else
+	return now_ns();
+#endif
 }
 
 static void batch_free(struct ixg_abatch *b)
@@ -139,6 +152,8 @@ int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
 	if (!a)
 		return -ENOMEM;
 	a->cfg = k;
+	a->tsc0 = tsc();
+	a->ns0 = now_ns();
 	/* a batch can always take one more frame of the largest size */
 	a->bytes_cap = (size_t)k.batch_bytes + IXG_MBUF_DATA_LEN;
 	c->async = a;
@@ -168,11 +183,17 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	else
 		ixg_stage_finish(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
 	const int direct = (a->cfg.flags & IXG_ASYNC_DIRECT) != 0;
+	const uint64_t t0 = tsc();
 	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, b->stream);
+	if (rc == 0 && hipEventRecord(b->done, b->stream) != hipSuccess)
+		rc = -EIO;
+	a->st.launch_ns += tsc() - t0;
 	if (rc)
 		return rc;
-	HIPCHK(hipEventRecord(b->done, b->stream));
 	b->state = AS_INFLIGHT;
+	a->st.batches++;
+	if (b->n < a->cfg.batch_frames && b->span < a->cfg.batch_bytes)
+		a->st.batches_by_time++;
 	return 0;
 }
 
@@ -229,6 +250,7 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 	}
 	const uint64_t t = now_ns();
 	uint32_t done = 0;
+	a->st.submit_calls++;
 	while (done < n) {
 		struct ixg_abatch *b = open_batch(a, t);
 		if (!b)
@@ -236,6 +258,7 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 		/* frames that fit the batch's count and byte limits (the last one
 		 * may pass the byte limit: bytes_cap leaves room for it) */
 		uint32_t m = 0;
+		const uint64_t g0 = tsc();
 		while (done + m < n && b->n + m < a->cfg.batch_frames && b->span < a->cfg.batch_bytes) {
 			/* at most as many frames as can still start below batch_bytes
 			 * (each stages at most IXG_MBUF_DATA_LEN - 12 bytes) */
@@ -253,6 +276,7 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 			memcpy(b->mbufs + b->n + m, mbufs + done + m, (size_t)take * sizeof(void *));
 			m += take;
 		}
+		a->st.gather_ns += tsc() - g0;
 		b->n += m;
 		done += m;
 		if (due(a, b, t)) {
@@ -267,6 +291,8 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 			}
 		}
 	}
+	a->st.frames_submitted += done;
+	a->st.frames_refused += n - done;
 	return (int)done;
 }
 
@@ -313,7 +339,10 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 		a->err = 0;
 		return e;
 	}
-	if (!a || !a->count || !max)
+	if (!a)
+		return 0;
+	a->st.poll_calls++;
+	if (!a->count || !max)
 		return 0;
 	HIPCHK(hipSetDevice(c->device));
 	/* an OPEN batch whose oldest frame has waited long enough goes now */
@@ -325,11 +354,19 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 				return rc;
 		}
 	}
+	const uint64_t p0 = tsc(); /* (after the launch: launch_ns has it) */
 	uint32_t got = 0;
 	while (a->count && got < max) {
 		struct ixg_abatch *b = &a->b[a->head];
 		if (b->state == AS_INFLIGHT) {
-			hipError_t e = (wait && got == 0) ? hipEventSynchronize(b->done) : hipEventQuery(b->done);
+			hipError_t e;
+			if (wait && got == 0) {
+				const uint64_t w0 = tsc();
+				e = hipEventSynchronize(b->done);
+				a->st.wait_ns += tsc() - w0;
+			} else {
+				e = hipEventQuery(b->done);
+			}
 			if (e == hipErrorNotReady)
 				break;
 			if (e != hipSuccess)
@@ -349,7 +386,34 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 			a->count--;
 		}
 	}
+	a->st.frames_returned += got;
+	a->st.poll_ns += tsc() - p0;
 	return (int)got;
+}
+
+int ixg_rx_async_stats(void *vctx, struct ixg_rx_async_stats *out, int reset)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c)
+		return -EINVAL;
+	struct ixg_async *a = c->async;
+	if (out) {
+		memset(out, 0, sizeof(*out));
+		if (a) {
+			*out = a->st;
+			/* ticks -> ns at the rate measured over the context's life */
+			const uint64_t dt = tsc() - a->tsc0, dn = now_ns() - a->ns0;
+			const double r = dt ? (double)dn / (double)dt : 1.0;
+			out->gather_ns = (uint64_t)((double)a->st.gather_ns * r);
+			out->launch_ns = (uint64_t)((double)a->st.launch_ns * r);
+			/* (poll_ns includes wait_ns) */
+			out->poll_ns = (uint64_t)((double)(a->st.poll_ns - a->st.wait_ns) * r);
+			out->wait_ns = (uint64_t)((double)a->st.wait_ns * r);
+		}
+	}
+	if (reset && a)
+		memset(&a->st, 0, sizeof(a->st));
+	return 0;
 }
 
 int ixg_rx_async_pending(void *vctx)

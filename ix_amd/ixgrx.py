@@ -50,6 +50,7 @@ EXPORTS = (
     "ixg_tx_set_macs", "ixg_tx_batch_dev", "ixg_tx_batch_host",
     "ixg_ev_batch_dev", "ixg_rx_set_split", "ixg_rx_set_fdir", "ixg_rx_launch_info",
     "ixg_rx_async_init", "ixg_rx_submit_mbufs", "ixg_rx_flush", "ixg_rx_poll", "ixg_rx_async_pending",
+    "ixg_rx_async_stats",
     "ixg_rx_register_memory", "ixg_rx_unregister_memory", "ixg_tcp_ext_batch_dev",
 )
 
@@ -71,6 +72,13 @@ class AsyncCfg(ctypes.Structure):
     """struct ixg_rx_async_cfg"""
     _fields_ = [("batch_frames", ctypes.c_uint32), ("batch_bytes", ctypes.c_uint32),
                 ("max_wait_us", ctypes.c_uint32), ("depth", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class AsyncStats(ctypes.Structure):
+    """struct ixg_rx_async_stats"""
+    _fields_ = [(k, ctypes.c_uint64) for k in (
+        "frames_submitted", "frames_returned", "frames_refused", "submit_calls", "poll_calls", "batches",
+        "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns")]
 
 
 IXG_ASYNC_DIRECT = 1 << 0
@@ -157,6 +165,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_poll.restype = i32
     lib.ixg_rx_async_pending.argtypes = [vp]
     lib.ixg_rx_async_pending.restype = i32
+    lib.ixg_rx_async_stats.argtypes = [vp, vp, i32]
+    lib.ixg_rx_async_stats.restype = i32
     lib.ixg_rx_register_memory.argtypes = [vp, vp, ctypes.c_size_t]
     lib.ixg_rx_register_memory.restype = i32
     lib.ixg_rx_unregister_memory.argtypes = [vp, vp]
@@ -300,6 +310,12 @@ class RxEngine:
         if rc < 0:
             _check(rc, "ixg_rx_async_pending", self._lib)
         return rc
+
+    def async_stats(self, reset: bool = False) -> dict:
+        """The asynchronous path's counters (ixg_rx_async_stats)."""
+        st = AsyncStats()
+        _check(self._lib.ixg_rx_async_stats(self._ctx, ctypes.byref(st), int(reset)), "ixg_rx_async_stats", self._lib)
+        return {k: int(getattr(st, k)) for k, _ in AsyncStats._fields_}
 
 
 def make_mbufs(tr) -> tuple[np.ndarray, np.ndarray]:

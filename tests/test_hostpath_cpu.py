@@ -292,3 +292,33 @@ def test_submit_launch_failure_keeps_accepted_frames(fake):
         eng.close()
     exp = _expect(ptrs[:100])
     assert np.array_equal(np.concatenate([r, r2]).view(np.uint8).reshape(-1, 16), exp)
+
+
+def test_async_stats_counters(fake):
+    """ixg_rx_async_stats: frames in and out, refusals under back-pressure,
+    batches launched full vs by time, and the time buckets filled."""
+    tr, arena, ptrs = _mbufs("tcp64", 640, seed=33)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=128, batch_bytes=1 << 20, max_wait_us=10000000, depth=2)
+        eng.async_stats(reset=True)
+        assert eng.submit_mbufs(ptrs[:64]) == 64
+        assert eng.submit_mbufs(ptrs[64:192]) == 128   # batch 1 full (launched), batch 2 open (64)
+        assert eng.submit_mbufs(ptrs[192:400]) == 64   # batch 2 full, ring full: 144 refused
+        st = eng.async_stats()
+        assert st["frames_submitted"] == 256 and st["frames_refused"] == 144 and st["submit_calls"] == 3
+        assert st["batches"] == 2 and st["batches_by_time"] == 0
+        m, r = eng.poll(1000, wait=True)
+        while eng.pending():
+            m2, r2 = eng.poll(1000, wait=True)
+            m = np.concatenate([m, m2])
+        assert eng.submit_mbufs(ptrs[256:300]) == 44
+        eng.flush()                                     # launched before full
+        m3, _ = eng.poll(1000, wait=True)
+        st = eng.async_stats(reset=True)
+        assert st["frames_returned"] == 300 and st["batches"] == 3 and st["batches_by_time"] == 1
+        assert st["gather_ns"] > 0 and st["launch_ns"] > 0 and st["poll_calls"] >= 3
+        assert eng.async_stats()["frames_submitted"] == 0   # reset
+    finally:
+        eng.close()
+    assert np.array_equal(np.concatenate([m, m3]), ptrs[:300])
