@@ -328,10 +328,11 @@ int ixg_rx_set_split(void *ctx, uint32_t split);
 /* How the context's last device-resident or host launch (ixg_rx_batch_dev,
  * ixg_rx_batch_host) split its batch, as the device decided it (DESIGN.md
  * 4.1): info[0] = IXG_MODE_* (0 fast, 1 short, 2 long; 0xffffffff when no
- * sampler ran), info[1] = 1 when the ring kernel took the launch, info[2] =
- * 1 when most sampled chunks were big. For tuning and tests; the caller
- * finishes the launch first (this call synchronizes only the context's own
- * stream). 0 or -errno. */
+ * sampler ran: coalesced fixed-stride batches, always fast), info[1] = 1
+ * when most sampled chunks were big (the long kernel then walks its chunks
+ * strided), info[2] = 1 when the sampling kernel ran. For tuning and tests;
+ * the caller finishes the launch first (this call synchronizes only the
+ * context's own stream). 0 or -errno. */
 int ixg_rx_launch_info(void *ctx, uint32_t info[3]);
 
 /* ---- host-side dispatch: the eth_input replacement ------------------- */

@@ -430,8 +430,8 @@ int ixg_rx_launch_info(void *vctx, uint32_t info[3])
 	HIPCHK(hipMemcpy(w, c->ds.d_present, sizeof(w), hipMemcpyDeviceToHost));
 	const int ran = c->ds.epoch != 0 && w[0] == c->ds.epoch;
 	info[0] = ran ? w[3] : 0xffffffffu;
-	info[1] = c->ds.epoch != 0 && w[7] == c->ds.epoch;
-	info[2] = ran && w[6] != 0;
+	info[1] = ran && w[6] != 0;
+	info[2] = (uint32_t)ran;
 	return 0;
 }
 

@@ -71,12 +71,6 @@ struct ixg_kparams {
 	uint32_t self_sample;  /* set by ixgrx_launch for the span-staged short
 	                          kernel when it runs first: it samples the
 	                          launch's mode itself and publishes it */
-	uint32_t ring;         /* set by ixgrx_launch when the ring kernel runs
-	                          before the long kernel: in a LONG-mode launch
-	                          the ring kernel takes every chunk it can stage
-	                          (present[7] == epoch then) and flags the rest
-	                          IXG_CLS_LONG for the long kernel */
-	uint32_t ring_slots;   /* the ring kernel's LDS ring, in 1 KiB slots */
 };
 
 /* the flow-director table's hash (host and device agree on it) */

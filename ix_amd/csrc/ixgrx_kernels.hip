@@ -1876,11 +1876,7 @@ DEV void general_body(const KParams& p) {
   // a block with no deferred chunk exits before staging the tables (the
   // common case behind the fixed-shape kernel: 64 B frames)
   const uint32_t mode = launch_mode(p);
-  // (LONG mode behind the ring kernel, which ran when present[7] holds the
-  // launch's epoch: only the chunks it flagged)
-  const bool all = CLS == IXG_CLS_SHORT
-                       ? mode == IXG_MODE_SHORT
-                       : (p.defer == nullptr || (mode == IXG_MODE_LONG && !(p.ring && p.present[7] == p.epoch)));
+  const bool all = CLS == IXG_CLS_SHORT ? mode == IXG_MODE_SHORT : (p.defer == nullptr || mode == IXG_MODE_LONG);
   // (p.present is only read when the flags are in use: it is null with
   // p.defer when the general kernel runs alone)
   if (!all) {
@@ -2203,443 +2199,6 @@ IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
 IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
 
 
-// ---- the ring kernel (C3: long chunks of packed batches) --------------------
-// One 1024-thread block per CU takes a contiguous range of chunks. Wave 0 is
-// the loader: for each chunk in order it copies the chunk's descriptor rows
-// (64 u64 offsets + 64 u16 lengths, one 1 KiB header slot) and its span of
-// frame bytes (floor16(first offset) .. last frame's end, whole 1 KiB slots)
-// HBM -> LDS with buffer_load ... lds (no VGPRs, the out-of-range part of a
-// piece reads 0) into a block-wide ring of 1 KiB slots, one chunk after the
-// other, as far ahead as the ring allows. The other 15 waves are consumers:
-// each takes the next chunk in order (an LDS ticket), waits until the loader
-// has published it landed, reads its frames' 96-byte prefixes and sums their
-// L4 tails [96, segment end) out of the ring (16-lane groups per frame,
-// medium segments first), gives the chunk's slots back, and only then parses
-// from registers and stores the records. The ring turns the walk's per-wave
-// HBM round trips (prefix, then 2-4 streaming rounds per chunk, each waiting
-// out the miss latency at 2 waves per SIMD) into one sequential stream per
-// CU with ~32 KiB always in flight.
-//
-// Protocol (all in LDS): queue entry e = seq % kRingQ holds the chunk's first
-// slot (a monotone slot counter), data slots, span base and bytes. The loader
-// writes the entry, issues its DMAs and, after a counted s_waitcnt vmcnt that
-// retires them, stores ready[e] = seq + 1 (the LDS-DMA data is ordered for
-// another wave's ds_read by the issuing wave's vmcnt; the ready store comes
-// after it, and the consumer's reads come after it sees the store). A
-// consumer stores done[e] = seq + 1 once its reads of the ring have returned.
-// The loader reuses slots only behind the oldest entry not yet done (in
-// order), and before it waits for space it retires and publishes everything
-// it has issued, so no consumer can wait on a chunk held back by the loader.
-// A chunk it cannot stage (span past kRingSpanMax, descending offsets) or
-// whose frames do not all lie in their span is flagged IXG_CLS_LONG for the
-// long kernel, which runs behind this one.
-constexpr int kRingWaves = 16;
-constexpr uint32_t kRingQ = 32;
-constexpr uint32_t kRingSpanMax = 40u * 1024u;  // bytes of one chunk's span the ring stages
-constexpr uint32_t kRingInflight = 32;          // DMA instructions the loader leaves in flight at a counted wait
-constexpr uint32_t kRingQD = 16;                // header queue slots (a chunk's descriptor rows)
-constexpr uint32_t kRingHdr = 640;              // bytes per header slot: 64 u64 offsets + 64 u16 lengths
-constexpr uint32_t kRingHA = 8;                 // headers issued this many chunks ahead of the data
-constexpr int kRingAux = 0;                     // cache policy of the ring's frame loads
-// s_waitcnt vmcnt(n) (gfx9 encoding: vmcnt[3:0] + [15:14]; expcnt, lgkmcnt at max)
-constexpr uint32_t vmcnt_imm(uint32_t n) { return (n & 15u) | ((n >> 4) << 14) | 0x0F70u; }
-
-constexpr int kRingLoaders = 2;                 // loader waves (waves 0 .. kRingLoaders-1)
-struct RingQ {
-  uint32_t pos[kRingQ];    // first data slot of the entry: a monotone slot counter
-  uint32_t npc[kRingQ];    // data slots (0: not staged)
-  uint32_t span[kRingQ];   // bytes of the span
-  uint32_t blo[kRingQ], bhi[kRingQ];  // batch offset of the span's first byte (16-aligned)
-  uint32_t ready[kRingLoaders][kRingQ];  // seq + 1 once the loader's share of the entry's DMAs landed
-  uint32_t done[kRingQ];   // seq + 1 once its consumer has finished reading the ring
-  uint32_t hready[kRingQD];  // seq + 1 once the chunk's header landed (loader 0 publishes it)
-  uint32_t ticket;         // consumers: the next seq to take
-};
-
-typedef __attribute__((address_space(3))) RingQ lds_ringq;
-
-DEV uint32_t lds_load(const lds_u32* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-DEV void lds_store(lds_u32* a, uint32_t v) { __hip_atomic_store(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
-
-// one 16-byte piece per lane, HBM -> LDS (dst: the wave's 1 KiB, lane l's 16 B at dst + 16 l)
-DEV void dma16(__amdgpu_buffer_rsrc_t r, lds_u32* dst, uint32_t voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)dst, 16, voff, 0, 0, kRingAux);
-}
-
-// An LDS word another wave writes, read by the loader. In inline asm with its
-// own lgkmcnt wait: hipcc cannot tell an LDS read from the ring's LDS-DMA
-// destinations (no alias scopes), so for a plain read it would first wait for
-// every DMA the loader has in flight (vmcnt(0)), i.e. drain the stream.
-DEV uint32_t lds_peek(const lds_u32* a) {
-  uint32_t v;
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(a) : "memory");
-  return __builtin_amdgcn_readfirstlane(v);
-}
-// ... and an LDS word the loader writes (for a plain store hipcc would wait for
-// every DMA in flight first: it might be one of their destinations)
-DEV void lds_poke(lds_u32* a, uint32_t v) { asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory"); }
-
-// s_waitcnt vmcnt(n) with n an immediate: the largest rung of the ladder
-// that is <= k (every DMA older than the k youngest has then landed).
-// Returns the rung waited for.
-DEV uint32_t vm_ladder(uint32_t k) {
-  if (k >= 48u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(48)); return 48u; }
-  if (k >= 32u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(32)); return 32u; }
-  if (k >= 16u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(16)); return 16u; }
-  if (k >= 8u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(8)); return 8u; }
-  if (k >= 4u) { __builtin_amdgcn_s_waitcnt(vmcnt_imm(4)); return 4u; }
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-  return 0u;
-}
-
-// The loader waves: chunks c0 .. c0 + nseq - 1 into the ring, in order. Each
-// of the kRingLoaders waves runs the same walk and issues its share of every
-// chunk's 1 KiB pieces (piece k: loader k mod kRingLoaders); one loader wave
-// alone tops out near 25 GB/s per CU (MI355X_MICROARCH.md ldsdma-fill), which
-// is C3's whole per-CU rate. Loader 0 also keeps every chunk's descriptor
-// rows (64 offsets + 64 lengths, 640 B) kRingHA chunks ahead in a header
-// queue of kRingQD slots and publishes each header once landed; the chunk's
-// span is read from it, so no loader has a load of its own to wait for (a
-// scalar load's lgkmcnt(0) also waits for whatever else is in flight on that
-// counter). Bookkeeping per queue entry stays in registers (lane e holds
-// entry e): first slot, DMA count after the header, after the loader's
-// share of the data. A loader waits on a DMA only when it needs it: the
-// header it is about to read, or, when the ring is full, the oldest chunk
-// it has not yet published.
-DEV void ring_loader(const KParams& p, lds_ringq* q, lds_u32* hq, lds_u32* ring, uint32_t NS, uint32_t c0,
-                     uint32_t nseq, int lane, uint32_t li) {
-  const uint32_t n = p.n;
-  uint32_t s = 0, hs = 0, pos = 0, wpos = 0, old = 0, pub = 0, issued = 0, landed = 0;
-  uint32_t vpos = 0, vhdr = 0, vend = 0;
-  auto rl = [](uint32_t v, uint32_t e) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(e % kRingQ)); };
-  auto publish = [&]() {
-    while (pub < s && rl(vend, pub) <= landed) {
-      lds_poke(&q->ready[li][pub % kRingQ], pub + 1u);
-      pub++;
-    }
-  };
-  auto wait_for = [&](uint32_t idx) {  // the DMA that brought the count to idx has landed
-    if (landed >= idx) return;
-    landed = issued - vm_ladder(issued - idx);
-    publish();
-  };
-  auto headers = [&]() {
-    while (li == 0u && hs < nseq && hs < s + kRingHA && hs - old < kRingQD) {
-      const uint32_t c = c0 + hs;
-      const uint32_t nv = n - c * 64u < 64u ? n - c * 64u : 64u;
-      lds_u32* h = hq + (hs % kRingQD) * (kRingHdr / 4u);
-      if (lane < 32) dma16(rsrc(p.off + (uint64_t)c * 64u, 8u * nv), h, 16u * (uint32_t)lane);
-      if (lane < 8) dma16(rsrc(p.len + (uint64_t)c * 64u, 2u * nv), h + 128, 16u * (uint32_t)lane);
-      issued += 2u;
-      vhdr = (uint32_t)lane == hs % kRingQ ? issued : vhdr;
-      hs++;
-    }
-  };
-  auto advance = [&]() {
-    while (old < s && lds_peek(&q->done[old % kRingQ]) == old + 1u) old++;
-  };
-  // nothing to issue yet: publish what has landed, oldest first (consumers
-  // free the ring only behind chunks every loader published), else sleep
-  auto idle = [&]() {
-    if (pub < s) {
-      wait_for(rl(vend, pub));
-    } else {
-      headers();
-      __builtin_amdgcn_s_sleep(1);
-    }
-  };
-  while (s < nseq) {
-    headers();
-    if (li == 0u) {
-      wait_for(rl(vhdr, s));
-      lds_poke(&q->hready[s % kRingQD], s + 1u);
-    } else {
-      while (lds_peek(&q->hready[s % kRingQD]) != s + 1u) idle();
-    }
-    const uint32_t c = c0 + s;
-    const uint32_t nv = n - c * 64u < 64u ? n - c * 64u : 64u;
-    const lds_u32* h = hq + (s % kRingQD) * (kRingHdr / 4u);
-    // the first offset, the last offset and the last length, one LDS round trip
-    uint64_t o0, o1;
-    uint32_t lw;
-    asm volatile("ds_read_b64 %0, %3\n\tds_read_b64 %1, %4\n\tds_read_b32 %2, %5\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&v"(o0), "=&v"(o1), "=&v"(lw)
-                 : "v"(h), "v"(h + 2u * (nv - 1u)), "v"(h + 128u + ((nv - 1u) >> 1))
-                 : "memory");
-    o0 = rfl64(o0);
-    o1 = rfl64(o1);
-    const uint32_t l1 = (__builtin_amdgcn_readfirstlane(lw) >> (16u * ((nv - 1u) & 1u))) & 0xffffu;
-    const uint64_t b16 = o0 & ~15ull, e = o1 + l1;
-    // (a batch's last chunk with a frame count that is not a multiple of 8
-    // has a descriptor piece half past the arrays: the long kernel takes it)
-    const bool stage = o1 >= o0 && e > b16 && e - b16 <= kRingSpanMax && (nv & 7u) == 0u;
-    const uint32_t span = stage ? (uint32_t)(e - b16) : 0u;
-    const uint32_t npc = (span + 1023u) >> 10;
-    // room: at most kRingQ entries, and the slots behind the oldest entry in use
-    for (;;) {
-      advance();
-      const uint32_t base = old < s ? rl(vpos, old) : pos;
-      if (s - old < kRingQ && pos + npc - base <= NS) break;
-      idle();
-    }
-    const uint32_t e_ = s % kRingQ;
-    if (li == 0u) {
-      lds_poke(&q->pos[e_], pos);
-      lds_poke(&q->npc[e_], npc);
-      lds_poke(&q->span[e_], span);
-      lds_poke(&q->blo[e_], (uint32_t)b16);
-      lds_poke(&q->bhi[e_], (uint32_t)(b16 >> 32));
-    }
-    // this loader's pieces of the span, one 1 KiB slot per wave instruction
-    // (whole 16-byte pieces: the last may run up to 15 bytes into the
-    // IXG_TAIL_PAD after the batch)
-    const __amdgpu_buffer_rsrc_t rd = rsrc(p.base + b16, (span + 15u) & ~15u);
-    uint32_t slot = wpos + li;
-    slot = slot >= NS ? slot - NS : slot;
-    uint32_t mine = 0;
-    for (uint32_t k = li; k < npc; k += kRingLoaders) {
-      dma16(rd, ring + slot * 256u, 1024u * k + 16u * (uint32_t)lane);
-      slot += kRingLoaders;
-      slot = slot >= NS ? slot - NS : slot;
-      mine++;
-    }
-    issued += mine;
-    vpos = (uint32_t)lane == e_ ? pos : vpos;
-    vend = (uint32_t)lane == e_ ? issued : vend;
-    s++;
-    pos += npc;
-    wpos += npc;
-    wpos = wpos >= NS ? wpos - NS : wpos;
-    if (issued - landed > kRingInflight) {
-      __builtin_amdgcn_s_waitcnt(vmcnt_imm(kRingInflight));
-      landed = issued - kRingInflight;
-      publish();
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(vmcnt_imm(0));
-  landed = issued;
-  publish();
-}
-
-// 4 dwords into a one's complement (end-around carry) accumulator
-DEV uint32_t adc4(uint32_t acc, const u32x4& a) {
-  asm volatile(
-      "v_add_co_u32 %0, vcc, %0, %1\n\t"
-      "v_addc_co_u32 %0, vcc, %0, %2, vcc\n\t"
-      "v_addc_co_u32 %0, vcc, %0, %3, vcc\n\t"
-      "v_addc_co_u32 %0, vcc, %0, %4, vcc\n\t"
-      "v_addc_co_u32 %0, vcc, %0, 0, vcc"
-      : "+v"(acc)
-      : "v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w)
-      : "vcc");
-  return acc;
-}
-
-typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-
-// DPP lane moves within rows of 16 (no LDS round trip, unlike ds_bpermute)
-template <int CTRL>
-DEV uint32_t dpp(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, false);
-}
-constexpr int kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
-
-// A consumer wave: chunks by ticket until the range is done. wl / ws: the
-// wave's 64-word LDS list and tail sums.
-template <bool DMX>
-DEV bool ring_consumer(const KParams& p, const Tab64& tab, const lds_u32* t6, lds_ringq* q, const lds_u32* hq,
-                       const lds_u32* ring, uint32_t NS, uint32_t c0, uint32_t nseq, lds_u32* wl, lds_u32* ws,
-                       int lane) {
-  const uint32_t R = NS * 1024u;
-  auto wrap = [&](uint32_t x) { return x >= R ? x - R : x; };
-  bool deferred = false;
-  for (;;) {
-    uint32_t t = 0;
-    if (lane == 0) t = __hip_atomic_fetch_add(&q->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    t = __builtin_amdgcn_readfirstlane(t);
-    if (t >= nseq) break;
-    const uint32_t e = t % kRingQ;
-    for (int l = 0; l < kRingLoaders; l++)
-      while (lds_load(&q->ready[l][e]) != t + 1u) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-    const uint32_t chunk = c0 + t;
-    const uint32_t pos = q->pos[e], npc = q->npc[e], span = q->span[e];
-    const uint64_t b16 = (uint64_t)q->blo[e] | ((uint64_t)q->bhi[e] << 32);
-    const lds_u32* hdr = hq + (t % kRingQD) * (kRingHdr / 4u);
-    const uint32_t i = chunk * 64u + (uint32_t)lane;
-    const bool valid = i < p.n;
-    const uint64_t off = (uint64_t)hdr[2 * lane] | ((uint64_t)hdr[2 * lane + 1] << 32);
-    const uint32_t L = valid ? (hdr[128 + (lane >> 1)] >> (16u * (uint32_t)(lane & 1))) & 0xffffu : 0u;
-    const uint64_t rel64 = off - b16;
-    const bool inside = !valid || L == 0u || (off >= b16 && rel64 + L <= span);
-    if (npc == 0u || !wave_all(inside)) {
-      // not staged: the long kernel behind this one takes the chunk
-      __builtin_amdgcn_s_waitcnt(kLdsWait);
-      if (lane == 0) {
-        lds_store(&q->done[e], t + 1u);
-        p.defer[chunk] = (uint8_t)IXG_CLS_LONG;
-      }
-      deferred = true;
-      continue;
-    }
-    // the frame's first byte in the ring
-    const uint32_t ra = wrap((pos % NS) * 1024u + (valid ? (uint32_t)rel64 : 0u));
-    // ---- phase R: everything read out of the ring ----
-    uint32_t d[kPrefixDw];
-    d[0] = d[1] = d[2] = 0;  // MAC addresses: never read
-    {
-      const uint32_t w0 = ra >> 2, R4 = R >> 2;
-      if (wave_all(ra + 4u * kPrefixDw <= R)) {
-        const lds_u32* f = ring + w0;
-#pragma unroll
-        for (int k = 3; k < kPrefixDw; k++) d[k] = f[k];
-      } else {
-#pragma unroll
-        for (int k = 3; k < kPrefixDw; k++) {
-          const uint32_t a = w0 + (uint32_t)k;
-          d[k] = ring[a >= R4 ? a - R4 : a];
-        }
-      }
-    }
-    // the L4 tail [96, segment end): the segment end as the parse will find
-    // it (IPv4: 14 + ip_len; IPv6 extension: 54 + payload length), summed
-    // for every frame the parse may stream (ip.c:87 / the IPv6 length check
-    // bound it by L); frames the parse does not stream ignore it
-    const uint32_t et = eth_type(d, L);
-    const bool six = (p.flags & IXG_F_IPV6) && et == 0x86DDu;
-    const uint32_t se = six ? 54u + ((byte_at(d, 18) << 8) | byte_at(d, 19)) : 14u + ((byte_at(d, 16) << 8) | byte_at(d, 17));
-    const bool cand = valid && (et == 0x0800u || six) && se > (uint32_t)kStreamBase && se <= L;
-    // ring-linear bounds (may pass R: wrapped at each read)
-    const uint32_t A = ra + (uint32_t)kStreamBase, E = ra + (cand ? se : (uint32_t)kStreamBase);
-    const uint32_t a16 = (A + 15u) & ~15u, e16 = E & ~15u;
-    // the owner's two partial pieces: [A, min(a16, E)) and [max(e16, a16), E)
-    uint32_t edge = 0;
-    {
-      const uint32_t hp = A & ~15u, tp = e16;
-      const u32x4 hv = *(const lds_u32x4*)(ring + (wrap(hp) >> 2));
-      const u32x4 tv = *(const lds_u32x4*)(ring + (wrap(tp) >> 2));
-      const uint32_t hh = a16 < E ? a16 : E;
-      uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, tw[4] = {tv.x, tv.y, tv.z, tv.w};
-      uint64_t es = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t xh = hp + 4u * (uint32_t)j, xt = tp + 4u * (uint32_t)j;
-        es += (xh >= A) ? keep_bytes(hw[j], (int)hh - (int)xh) : 0u;
-        es += (tp >= a16) ? keep_bytes(tw[j], (int)E - (int)xt) : 0u;
-      }
-      edge = cand ? fold32(es) : 0u;
-    }
-    // whole pieces [a16, e16): medium segments (<= 32 pieces) by 4-lane
-    // groups, longer ones by 16-lane groups, packed over the wave's lanes
-    // (medium entries first, long ones from a 16-aligned lane on), 64 lanes
-    // per round; every lane issues its (up to 8) piece reads at once, then
-    // sums them, then the group folds its lanes together by DPP
-    const uint32_t npi = cand && e16 > a16 ? (e16 - a16) >> 4 : 0u;
-    const bool med = npi != 0u && npi <= 32u;
-    const uint64_t mmed = __ballot(med), mlng = __ballot(npi > 32u);
-    const uint32_t nmed = (uint32_t)__popcll(mmed), nlng = (uint32_t)__popcll(mlng);
-    if (npi) {
-      // the entry: {owner lane | pieces << 8, first piece's ring address}
-      const uint64_t mine = med ? mmed : mlng;
-      const uint32_t at = (med ? 0u : nmed) +
-                          __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0u));
-      typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-      *(__attribute__((address_space(3))) u32x2v*)(wl + 2u * at) = u32x2v{(uint32_t)lane | (npi << 8), a16};
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t lstart = (4u * nmed + 15u) & ~15u, total = lstart + 16u * nlng;
-    for (uint32_t v0 = 0; v0 < total; v0 += 64u) {
-      const uint32_t v = v0 + (uint32_t)lane;
-      const bool big = v >= lstart;
-      const uint32_t G = big ? 16u : 4u;
-      const uint32_t k = big ? nmed + ((v - lstart) >> 4) : v >> 2;
-      const bool act = big ? v < total : k < nmed;
-      const uint32_t gl = v & (G - 1u);
-      typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
-      const u32x2v ent = *(const __attribute__((address_space(3))) u32x2v*)(wl + 2u * (act ? k : 0u));
-      const uint32_t owner = ent.x & 63u, oa = ent.y, on = act ? ent.x >> 8 : 0u;
-      uint32_t acc = 0;
-      for (uint32_t j0 = gl; wave_any(j0 < on); j0 += 8u * G) {
-        u32x4 pv[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const uint32_t j = j0 + G * (uint32_t)u;
-          pv[u] = *(const lds_u32x4*)(ring + (wrap(oa + 16u * (j < on ? j : 0u)) >> 2));
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const uint32_t m = 0u - (uint32_t)(j0 + G * (uint32_t)u < on);
-          acc = adc4(acc, u32x4{pv[u].x & m, pv[u].y & m, pv[u].z & m, pv[u].w & m});
-        }
-      }
-      acc = add1c(acc, dpp<kDppQuadXor1>(acc));
-      acc = add1c(acc, dpp<kDppQuadXor2>(acc));
-      const uint32_t s8 = add1c(acc, dpp<kDppHalfMirror>(acc));
-      const uint32_t s16 = add1c(s8, dpp<kDppMirror>(s8));
-      acc = big ? s16 : acc;
-      if (act && gl == 0u) ws[owner] = acc;
-    }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t tail = npi ? add1c(edge, ws[lane]) : edge;
-    // every read of the ring has returned: the slots go back to the loader
-    __builtin_amdgcn_s_waitcnt(kLdsWait);
-    if (lane == 0) lds_store(&q->done[e], t + 1u);
-    // ---- phase P: parse, records ----
-    if (lane == 0) p.defer[chunk] = 0;
-    LaneState st;
-    parse_dispatch(p, tab, d, L, valid, st, t6);
-    uint32_t r4 = l4_residual(st);
-    if (st.stream) r4 = (~fold16(add1c(fold32(st.l4_acc), tail))) & 0xffffu;
-    if (valid) {
-      const Rec r = make_record(p, d, L, st, r4);
-      store_record(p, i, r, st.ip_res, r4);
-      store_demux<DMX>(p, i, r, st.src, st.dst, st.ports);
-    }
-  }
-  return deferred;
-}
-
-// LONG-mode launches of packed u64-offset batches (not mostly big chunks):
-// the ring takes every chunk. Any other launch: exits at once (block 0
-// records that in present[7], which the long kernel reads).
-extern "C" __global__ void __launch_bounds__(64 * kRingWaves) ixg_rx_ring_o(KParams p) {
-  __shared__ uint64_t T[12 * 256];
-  __shared__ RingQ q;
-  __shared__ uint32_t sh_l[kRingWaves][128], sh_s[kRingWaves][64];
-  extern __shared__ u32x4 dynr[];  // [IPv6 tables (IXG_F_IPV6)] then the ring
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const bool run = launch_mode(p) == IXG_MODE_LONG && !launch_big(p);
-  if (blockIdx.x == 0 && threadIdx.x == 0) p.present[7] = run ? p.epoch : 0u;
-  if (!run) return;
-  const uint32_t nchunks = (p.n + 63u) >> 6;
-  const uint32_t c0 = (uint32_t)((uint64_t)nchunks * blockIdx.x / gridDim.x);
-  const uint32_t c1 = (uint32_t)((uint64_t)nchunks * (blockIdx.x + 1) / gridDim.x);
-  const uint32_t nseq = c1 - c0;
-  const uint32_t t6w = p.tab6 ? IXG_TAB6_WORDS : 0u;
-  if (p.tab6) {
-    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kRingWaves)
-      dynr[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
-  }
-  lds_ringq* lq = (lds_ringq*)&q;
-  for (int k = threadIdx.x; k < (int)kRingQ; k += 64 * kRingWaves) {
-    for (int l = 0; l < kRingLoaders; l++) lq->ready[l][k] = 0u;
-    lq->done[k] = 0u;
-    if (k < (int)kRingQD) lq->hready[k] = 0u;
-  }
-  if (threadIdx.x == 0) lq->ticket = 0u;
-  stage_tables(p, T);  // (ends with the block barrier)
-  lds_u32* hq = LDS(lds_u32, dynr) + t6w;
-  lds_u32* ring = hq + kRingQD * kRingHdr / 4u;
-  const uint32_t NS = p.ring_slots;
-  bool deferred = false;
-  if (wave < kRingLoaders)
-    ring_loader(p, lq, hq, ring, NS, c0, nseq, lane, (uint32_t)wave);
-  else
-    deferred = ring_consumer<false>(p, Tab64{T}, LDS(const lds_u32, dynr), lq, hq, ring, NS, c0, nseq,
-                                    LDS(lds_u32, sh_l[wave]), LDS(lds_u32, sh_s[wave]), lane);
-  if (deferred && lane == 0) p.present[IXG_CLS_LONG] = p.epoch;
-}
-
 // The sampler: one block picks the launch's IXG_MODE_*: FAST when at least
 // half of the sampled chunks could be fixed-shape by length (every frame <=
 // 64 B), else SHORT when at least half are short, else LONG.
@@ -2683,31 +2242,6 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
   const uint64_t cap = (uint64_t)ncu * (uint64_t)occupancy(k, shmem, block);
   const uint64_t g = want < cap ? want : cap;
   return g ? (uint32_t)g : 1u;
-}
-
-// The ring kernel's slots: the LDS its block leaves after its static arrays
-// and the dynamic IPv6 tables (sh6 bytes), 1 KiB each (0: cannot launch)
-static uint32_t ring_slots(size_t sh6) {
-  static std::mutex mu;
-  static int stat = -1;
-  static size_t set_for = ~(size_t)0;
-  std::lock_guard<std::mutex> lock(mu);
-  if (stat < 0) {
-    hipFuncAttributes a;
-    if (hipFuncGetAttributes(&a, reinterpret_cast<const void*>(ixg_rx_ring_o)) != hipSuccess) return 0;
-    stat = (int)a.sharedSizeBytes;
-  }
-  const size_t lds = 160u * 1024u, hq = (size_t)kRingQD * kRingHdr;
-  if ((size_t)stat + sh6 + hq + 48u * 1024u > lds) return 0;
-  const uint32_t ns = (uint32_t)((lds - (size_t)stat - sh6 - hq) / 1024u);
-  const size_t dyn = sh6 + hq + 1024u * ns;
-  if (set_for != dyn) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(ixg_rx_ring_o), hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)dyn) != hipSuccess)
-      return 0;
-    set_for = dyn;
-  }
-  return ns;
 }
 
 // The launch plan: coalesced fixed strides <= 64 B
@@ -2761,10 +2295,6 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
   // coalesced batches in the default split: the coalesced kernel finished
   // every chunk itself
   if (p.defer && coal && p.force_mode == IXG_MODE_AUTO) return (int)hipGetLastError();
-  // the ring kernel (LONG-mode launches of packed offset batches in device
-  // memory): 16-B aligned frames, offsets and lengths for its 16-byte DMAs
-  const bool ring = self && lay == 1 && !p.host_mem && ((reinterpret_cast<uintptr_t>(p.base) |
-                    reinterpret_cast<uintptr_t>(p.off) | reinterpret_cast<uintptr_t>(p.len)) & 15u) == 0u;
   if (p.defer) {
     const ShortK& ks = p.dmx ? k_short_dmx : k_short;
     // one wave per 64 chunks (frames in host memory: one per chunk)
@@ -2775,21 +2305,9 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
                        (hipStream_t)stream, ps);
   }
-  KParams pg = p;
-  if (ring) {
-    const uint32_t ns = ring_slots(sh6);
-    if (ns) {
-      pg.ring = 1u;
-      pg.ring_slots = ns;
-      const uint64_t g = nchunks < ncu ? nchunks : ncu;
-      hipLaunchKernelGGL(ixg_rx_ring_o, dim3((uint32_t)(g ? g : 1u)), dim3(64 * kRingWaves),
-                         sh6 + (size_t)kRingQD * kRingHdr + 1024u * ns,
-                         (hipStream_t)stream, pg);
-    }
-  }
   const kern_fn kg = k_gen[lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, p.host_mem ? wave_blocks : group_blocks, ncu, sh6)), dim3(kBlock), sh6,
-                     (hipStream_t)stream, pg);
+                     (hipStream_t)stream, p);
   return (int)hipGetLastError();
 }
 

@@ -219,7 +219,7 @@ class RxEngine:
         info = np.zeros(3, dtype=np.uint32)
         _check(self._lib.ixg_rx_launch_info(self._ctx, info.ctypes.data), "ixg_rx_launch_info", self._lib)
         modes = {0: "fast", 1: "short", 2: "long"}
-        return {"mode": modes.get(int(info[0])), "ring": bool(info[1]), "big": bool(info[2])}
+        return {"mode": modes.get(int(info[0]), "fast"), "big": bool(info[1]), "sampled": bool(info[2])}
 
     def set_fdir(self, filters, cpu_id: int = 0) -> None:
         """Flow-director perfect filters (FDIR_DTYPE array; empty = none)."""
