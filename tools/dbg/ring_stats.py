@@ -33,4 +33,5 @@ for wname in sys.argv[1:] or ["c3"]:
     print(f"{wname}: {ms:.4f} ms/launch; per loader wave per launch: total {v[0]/nl:.0f} cyc, "
           f"blocked {v[1]/nl:.0f} ({v[3]/nl:.0f} spins), header waits {v[2]/nl:.0f}; "
           f"per chunk: ready wait {v[4]/max(v[7],1):.0f}, phase R {v[5]/max(v[7],1):.0f}, phase P {v[6]/max(v[7],1):.0f} cyc; "
-          f"chunks {v[7]/K:.0f} (of {nchunks/K:.0f}); consumer wave total {v[8]/max(v[9],1):.0f} cyc")
+          f"chunks {v[7]/K:.0f} (of {nchunks/K:.0f}); consumer wave total {v[8]/max(v[9],1):.0f} cyc; "
+          f"phase R parts: header {v[11]/max(v[7],1):.0f}, prefix+edges {v[12]/max(v[7],1):.0f}, tails {v[13]/max(v[7],1):.0f}")

@@ -45,9 +45,7 @@ rep("""    for (int l = 0; l < kRingLoaders; l++)
     for (int l = 0; l < kRingLoaders; l++)
       while (lds_load(&q->ready[l][e]) != t + 1u) __builtin_amdgcn_s_sleep(1);
     uint64_t r1_ = __builtin_amdgcn_s_memtime(); trd += r1_ - r0_; nch++;""")
-rep("""    if (lane == 0) lds_store(&q->done[e], t + 1u);
-    // ---- phase P: parse, records ----""", """    if (lane == 0) lds_store(&q->done[e], t + 1u);
-    uint64_t r2_ = __builtin_amdgcn_s_memtime(); tR += r2_ - r1_;
+rep("""    // ---- phase P: parse, records ----""", """    uint64_t r2_ = __builtin_amdgcn_s_memtime(); tR += r2_ - r1_;
     // ---- phase P: parse, records ----""")
 rep("""      store_demux<DMX>(p, i, r, st.src, st.dst, st.ports);
     }
@@ -65,4 +63,19 @@ rep("""extern "C" uint32_t ixgrx_kparams_size(void)""", """extern "C" int ixgrx_
   return 0;
 }
 extern "C" uint32_t ixgrx_kparams_size(void)""")
+out = t
+# phase R sub-phases: header + inside check, prefix + edges, tail rounds
+t = t.replace("    const uint32_t ra = wrap((pos % NS) * 1024u + (valid ? (uint32_t)rel64 : 0u));",
+              "    const uint32_t ra = wrap((pos % NS) * 1024u + (valid ? (uint32_t)rel64 : 0u));\n"
+              "    uint64_t s1_ = __builtin_amdgcn_s_memtime(); tH_ += s1_ - r1_;", 1)
+t = t.replace("    // whole pieces [a16, e16): medium segments (<= 32 pieces) by 4-lane",
+              "    uint64_t s2_ = __builtin_amdgcn_s_memtime(); tPE_ += s2_ - s1_;\n"
+              "    // whole pieces [a16, e16): medium segments (<= 32 pieces) by 4-lane", 1)
+t = t.replace("    const uint32_t tail = npi ? add1c(edge, ws[lane]) : edge;",
+              "    const uint32_t tail = npi ? add1c(edge, ws[lane]) : edge;\n"
+              "    tT_ += __builtin_amdgcn_s_memtime() - s2_;", 1)
+t = t.replace("  uint64_t trd = 0, tR = 0, tP = 0, nch = 0, tw0 = __builtin_amdgcn_s_memtime();",
+              "  uint64_t trd = 0, tR = 0, tP = 0, nch = 0, tw0 = __builtin_amdgcn_s_memtime(), tH_ = 0, tPE_ = 0, tT_ = 0;", 1)
+t = t.replace("RST(8, __builtin_amdgcn_s_memtime() - tw0); RST(9, 1); }",
+              "RST(8, __builtin_amdgcn_s_memtime() - tw0); RST(9, 1); RST(11, tH_); RST(12, tPE_); RST(13, tT_); }", 1)
 out = t

@@ -16,6 +16,7 @@
 #   profile          the round profile: kernel trace of the default bench, PMC traffic (tools/profile_round.sh)
 #   ab:W:L1,L2,...   same-process A/B of library builds over workload W (tools/ab_lib.py; tools/build_variant.sh)
 #   py:SCRIPT,A,...  python3 SCRIPT A ... (a probe or a one-off measurement) -> py_<i>.log
+#   sqlib:W:LIB      SQ counter passes of one workload through a library build (tools/dbg/run_lib.py)
 set -o pipefail
 TAG=${1:?tag}; shift
 O=gpurun_out/$TAG
@@ -50,6 +51,13 @@ for STEP in "$@"; do
     profile) timeout -k 10 1000 bash tools/profile_round.sh "$TAG/profile" ;;
     ab) timeout -k 10 900 python3 -u tools/ab_lib.py --workload "${arg%%:*}" --libs "${arg#*:}" > "$O/ab_$i.json" 2> "$O/ab_$i.log" ;;
     py) timeout -k 10 600 python3 -u $args > "$O/py_$i.log" 2>&1 ;;
+    sqlib)
+      w=${arg%%:*}; lib=${arg#*:}; d="$O/sqlib_$i"; mkdir -p "$d"
+      P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU"
+      P2="SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM"
+      timeout -k 10 120 rocprofv3 --pmc $P1 --output-format csv -d "$d/${w}_p1" -o p -- python3 tools/dbg/run_lib.py "$lib" "$w" > "$d/p1.log" 2>&1 &&
+      timeout -k 10 120 rocprofv3 --pmc $P2 --output-format csv -d "$d/${w}_p2" -o p -- python3 tools/dbg/run_lib.py "$lib" "$w" > "$d/p2.log" 2>&1 &&
+      python3 tools/sq_report.py "$d" "$w" > "$O/sqlib_$i.txt" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
   rc=$?
