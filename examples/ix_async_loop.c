@@ -326,7 +326,7 @@ static int run_loop(void)
 	}
 	/* the per-thread breakdown, summed over threads (ns per frame of each
 	 * part of a thread's time; the rest is the loop itself and waiting) */
-	double g_ns = 0, l_ns = 0, p_ns = 0, w_ns = 0, d_s = 0, gap = 0;
+	double g_ns = 0, l_ns = 0, p_ns = 0, w_ns = 0, d_s = 0, gap = 0, lmax = 0;
 	uint64_t batches = 0, by_time = 0, refused = 0, offered = 0;
 	long vcs = 0, ivcs = 0;
 	for (int i = 0; i < opt.threads; i++) {
@@ -344,6 +344,8 @@ static int run_loop(void)
 		ivcs += ws[i].nivcsw;
 		if (ws[i].max_gap > gap)
 			gap = ws[i].max_gap;
+		if ((double)a->launch_max_ns > lmax)
+			lmax = (double)a->launch_max_ns;
 	}
 	const double fr = frames ? (double)frames : 1.0;
 	double *lat = malloc((nl ? nl : 1) * sizeof(double));
@@ -374,7 +376,7 @@ static int run_loop(void)
 	       "\"breakdown\": {\"thread_ns_per_frame\": %.2f, \"gather_ns_per_frame\": %.2f, \"launch_us_per_batch\": %.2f, "
 	       "\"poll_ns_per_frame\": %.2f, \"wait_ns_per_frame\": %.2f, \"dispatch_ns_per_frame\": %.2f, "
 	       "\"frames_per_batch\": %.0f, \"batches_by_time\": %.3f, \"refused_share\": %.3f, "
-	       "\"max_loop_gap_us\": %.1f, \"context_switches\": {\"voluntary\": %ld, \"involuntary\": %ld}}}\n",
+	       "\"max_loop_gap_us\": %.1f, \"max_launch_us\": %.1f, \"context_switches\": {\"voluntary\": %ld, \"involuntary\": %ld}}}\n",
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
 	       nl ? lat[nl - 1] : 0.0, nl, staged_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
@@ -383,7 +385,7 @@ static int run_loop(void)
 	       (unsigned long long)st.drop, el * opt.threads * 1e9 / fr, g_ns / fr,
 	       batches ? l_ns / (double)batches / 1e3 : 0.0, p_ns / fr, w_ns / fr, d_s * 1e9 / fr,
 	       batches ? fr / (double)batches : 0.0, batches ? (double)by_time / (double)batches : 0.0,
-	       offered ? (double)refused / (double)offered : 0.0, gap * 1e6, vcs, ivcs);
+	       offered ? (double)refused / (double)offered : 0.0, gap * 1e6, lmax / 1e3, vcs, ivcs);
 	if (opt.dump) {
 		FILE *f = fopen(opt.dump, "wb");
 		if (!f || fwrite(ws[0].dump, sizeof(struct ixg_rx_rec), ws[0].ndump, f) != ws[0].ndump)

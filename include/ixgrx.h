@@ -244,22 +244,26 @@ struct ixg_rx_async_stats {
 	uint64_t batches;          /* launched */
 	uint64_t batches_by_time;  /* ... of which before they were full (max_wait_us passed, flush, poll with wait) */
 	uint64_t gather_ns;        /* submit: copying frames into the pinned staging */
-	uint64_t launch_ns;        /* enqueuing batches: copies, kernels, event */
-	uint64_t poll_ns;          /* poll: event queries and copying records out */
+	uint64_t launch_ns;        /* enqueuing batches: copies, kernels, completion stamp */
+	uint64_t poll_ns;          /* poll: completion checks and copying records out */
 	uint64_t wait_ns;          /* poll with wait != 0: blocked on the GPU */
+	uint64_t launch_max_ns;    /* the longest single batch launch */
 };
 /* Copy the counters to *out (may be NULL) and, reset != 0, zero them. 0 or -errno. */
 int ixg_rx_async_stats(void *ctx, struct ixg_rx_async_stats *out, int reset);
 
 /* Zero copy: make host memory that holds mbufs (IX's mbuf mempool, its 2 MB
  * pages, dp/core/mempool.c:198-243) readable by the kernels (page-locked and
- * mapped, hipHostRegister). With IXG_ASYNC_DIRECT, a submitted frame whose
- * whole mbuf plus IXG_TAIL_PAD bytes lies inside a registered region is then
- * not gathered: the kernels read it where it is, over the host link, and the
- * CPU only stages its pointer and length. Frames outside every region are
- * gathered as before. Up to 32 regions per context, none overlapping; they
+ * mapped, hipHostRegister). With IXG_ASYNC_DIRECT, a submitted frame of at
+ * least IXG_ZC_MIN_LEN bytes whose whole mbuf plus IXG_TAIL_PAD bytes lies
+ * inside a registered region is then not gathered: the kernels read it where
+ * it is, over the host link, and the CPU only stages its pointer and length.
+ * Shorter frames, and frames outside every region, are gathered as before
+ * (a short frame costs the CPU a few ns to copy, while the kernels' reads
+ * of it in place cost host-link requests: DESIGN.md 5). Up to 32 regions per context, none overlapping; they
  * stay registered until ixg_rx_unregister_memory (-EBUSY while frames are
  * pending) or ixg_rx_fini. 0 or -errno. */
+#define IXG_ZC_MIN_LEN 256u
 int ixg_rx_register_memory(void *ctx, void *base, size_t bytes);
 int ixg_rx_unregister_memory(void *ctx, void *base);
 

@@ -565,7 +565,9 @@ size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos,
 		size_t l;
 		memcpy(&l, mb, sizeof(l)); /* mbuf->len (inc/ix/mbuf.h:75) */
 		len[k] = (uint16_t)l;
-		uint32_t r = 0;
+		/* frames shorter than IXG_ZC_MIN_LEN are gathered (cheaper than the
+		 * kernels' host-link reads of them in place) */
+		uint32_t r = l < IXG_ZC_MIN_LEN ? c->nreg : 0;
 		/* the mbuf and the bytes the kernels may read past its frame inside
 		 * the region (ixg_rx_register_memory) */
 		while (r < c->nreg && !(a >= c->reg[r].lo && a + IXG_MBUF_STRIDE + IXG_TAIL_PAD <= c->reg[r].hi))

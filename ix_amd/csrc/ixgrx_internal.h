@@ -133,6 +133,9 @@ IXG_HD static inline uint32_t ixg_demux_group(uint32_t fg_id, uint32_t fg_base, 
  * kernel; grids are sized from the device's CU count and each kernel's
  * occupancy */
 int ixgrx_launch(const void *params, uint32_t ncu, void *stream);
+/* enqueue the completion stamp: *flag = v (coherent pinned host memory), after
+ * everything enqueued before it on the stream */
+int ixgrx_stamp(uint32_t *flag, uint32_t v, void *stream);
 uint32_t ixgrx_kparams_size(void);
 uint32_t ixgrx_block(void);
 

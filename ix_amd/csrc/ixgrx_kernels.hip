@@ -2244,6 +2244,19 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
   return g ? (uint32_t)g : 1u;
 }
 
+// The asynchronous host path's completion stamp (ixgrx_async.c): after
+// everything enqueued before it on the stream, one lane stores v to a word of
+// coherent pinned host memory with a system-scope release, so the host sees
+// a finished batch by reading that word (no runtime call, no runtime lock)
+extern "C" __global__ void __launch_bounds__(64) ixg_done_stamp(uint32_t* f, uint32_t v) {
+  if (threadIdx.x == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+extern "C" int ixgrx_stamp(uint32_t* flag, uint32_t v, void* stream) {
+  hipLaunchKernelGGL(ixg_done_stamp, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, v);
+  return (int)hipGetLastError();
+}
+
 // The launch plan: coalesced fixed strides <= 64 B
 // (16-B aligned base) take the coalesced fixed-shape kernel alone; other
 // layouts the span-staged short kernel, which samples the mode itself, then

@@ -78,10 +78,11 @@ class AsyncStats(ctypes.Structure):
     """struct ixg_rx_async_stats"""
     _fields_ = [(k, ctypes.c_uint64) for k in (
         "frames_submitted", "frames_returned", "frames_refused", "submit_calls", "poll_calls", "batches",
-        "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns")]
+        "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns", "launch_max_ns")]
 
 
 IXG_ASYNC_DIRECT = 1 << 0
+IXG_ZC_MIN_LEN = 256  # registered frames shorter than this are gathered anyway
 ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=4 << 20, max_wait_us=50, depth=2, direct=True)
 
 

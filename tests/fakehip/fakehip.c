@@ -28,7 +28,7 @@
 #include "../../ix_amd/csrc/ixgrx_internal.h"
 #include "../../oracle/ixgrx_oracle.h"
 
-enum { OP_COPY, OP_SET, OP_RX, OP_MARK };
+enum { OP_COPY, OP_SET, OP_RX, OP_MARK, OP_STAMP };
 
 struct op {
 	int kind;
@@ -141,6 +141,9 @@ static void run_op(struct op *o)
 	}
 	case OP_MARK:
 		o->ev->s = NULL;
+		break;
+	case OP_STAMP:
+		__atomic_store_n((uint32_t *)o->dst, (uint32_t)o->val, __ATOMIC_RELEASE);
 		break;
 	}
 }
@@ -349,6 +352,18 @@ int ixgrx_launch(const void *params, uint32_t ncu, void *stream)
 	struct op *o = new_op(OP_RX);
 	memcpy(&o->p, params, sizeof(o->p));
 	o->fdir_sum = fdir_sum(o->p.fdir);
+	push((hipStream_t)stream, o);
+	return 0;
+}
+/* the completion stamp: written when the stream runs up to it (a poll that
+ * reads the word before someone synchronizes sees the batch unfinished) */
+int ixgrx_stamp(uint32_t *flag, uint32_t v, void *stream)
+{
+	if (!reachable((uintptr_t)flag, (uintptr_t)(flag + 1)))
+		abort();
+	struct op *o = new_op(OP_STAMP);
+	o->dst = flag;
+	o->val = (int)v;
 	push((hipStream_t)stream, o);
 	return 0;
 }

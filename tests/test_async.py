@@ -178,7 +178,7 @@ def test_sync_mbuf_path_skips_macs():
         assert np.array_equal(r2, r1), kind
 
 
-@pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed"])
+@pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed", "tcp1514"])
 def test_zero_copy_registered_mbufs(kind):
     """Registered mbuf memory: the kernels read the frames in place over the
     host link (no gather); a third of the frames come from an unregistered

@@ -198,11 +198,12 @@ def test_async_rejects_oversized_and_bad_cfg(fake):
         eng.close()
 
 
-@pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed"])
+@pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed", "tcp1514"])
 def test_async_zero_copy(fake, kind):
-    """Registered mbuf memory (ixg_rx_register_memory): frames are read in
-    place, nothing of them is gathered; frames of unregistered mbufs in the
-    same batches are gathered; records as the oracle's, in order."""
+    """Registered mbuf memory (ixg_rx_register_memory): frames of at least
+    IXG_ZC_MIN_LEN bytes are read in place, nothing of them is gathered;
+    shorter ones, and frames of unregistered mbufs in the same batches, are
+    gathered; records as the oracle's, in order."""
     fake.lib.fakehip_inplace_frames.restype = ctypes.c_ulong
     rng = np.random.default_rng(21)
     tr, arena, ptrs = _mbufs(kind, 6000, seed=13)
@@ -216,15 +217,18 @@ def test_async_zero_copy(fake, kind):
             eng.register_memory(arena.ctypes.data + 4096, 1 << 16)  # overlaps
         n0 = fake.lib.fakehip_inplace_frames()
         m, r = _loop(eng, ptrs, rng)
-        # every frame whose mbuf (and the tail bytes) lies inside the region is read in place
+        # every frame of >= IXG_ZC_MIN_LEN bytes whose mbuf (and the tail
+        # bytes) lies inside the region is read in place
         hi = arena.ctypes.data + arena.nbytes
-        inside = (ptrs.astype(np.int64) + 2112 + 64 <= hi)
-        assert fake.lib.fakehip_inplace_frames() - n0 == int(inside.sum()) >= len(ptrs) - 1
+        big = tr.len.astype(np.int64) >= ixgrx.IXG_ZC_MIN_LEN
+        inside = (ptrs.astype(np.int64) + 2112 + 64 <= hi) & big
+        assert fake.lib.fakehip_inplace_frames() - n0 == int(inside.sum()) >= int(big.sum()) - 1
+        assert kind not in ("imix", "tcp1514") or inside.sum() > 0
         assert np.array_equal(m, ptrs)
         assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
         n1 = fake.lib.fakehip_inplace_frames()
         m, r = _loop(eng, mix, rng)
-        assert fake.lib.fakehip_inplace_frames() - n1 == int(((mix == ptrs) & (mix.astype(np.int64) + 2176 <= hi)).sum())
+        assert fake.lib.fakehip_inplace_frames() - n1 == int(((mix == ptrs) & (mix.astype(np.int64) + 2176 <= hi) & big).sum())
         assert np.array_equal(m, mix)
         assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(mix))
         eng.unregister_memory(arena.ctypes.data)
