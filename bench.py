@@ -298,9 +298,9 @@ def parity_leg(checks, key) -> dict:
             er, _ = oracle.rx_trace(pool, key, flags=flags, threads=8, hash_mode=oracle.HASH_TABLE)
             res[name] = "ok" if tiled and np.array_equal(rec, er) else "MISMATCH"
         elif c[0] == "hostpath":
-            _, pool, recs = c
+            _, pool, recs, name = c
             er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
-            res["hostpath"] = "ok" if np.array_equal(recs, er) else "MISMATCH"
+            res[name] = "ok" if np.array_equal(recs, er) else "MISMATCH"
         elif c[0] == "mbufs":
             _, tr, ptrs, arena, rec = c
             er = oracle.rx_mbufs(key, 128, 0, 0, ptrs[:1 << 16], threads=8, hash_mode=oracle.HASH_TABLE)
@@ -719,11 +719,15 @@ def host_path(seconds: float = 3.0, threads=(1, 4, 16)):
     RX queue, dp/core/ethqueue.c:71,117-149) drives libixgrx's asynchronous
     host path, one context per host thread (IX's per-CPU model), over C2's
     64-B frames in 2112-B IX mbufs: aggregate Mpkt/s and submit->poll
-    latency at 1/4/16 threads, next to cpu_baseline. Beside it, the latency
-    of one synchronous ixg_rx_batch_mbufs call at n = 64 / 1K / 64K frames
-    and of one 64-frame batch through the asynchronous path (staged copies,
-    and IXG_ASYNC_DIRECT: kernels on pinned host memory). Thread 0's first
-    pass of the loop is kept for the oracle check."""
+    latency at 1/4/16 threads, next to cpu_baseline, with the library's
+    per-thread breakdown (ixg_rx_async_stats). Then 1514-B frames at 16
+    threads, gathered and read in place from registered mbuf memory (zero
+    copy: ixg_rx_register_memory; frames under IXG_ZC_MIN_LEN are gathered
+    anyway, so C2's frames never take it). Beside them, the latency of one
+    synchronous ixg_rx_batch_mbufs call at n = 64 / 1K / 64K frames and of
+    one 64-frame batch through the asynchronous path (staged copies, and
+    IXG_ASYNC_DIRECT: kernels on pinned host memory). Thread 0's first pass
+    of the C2 loop and of the zero-copy loop are kept for the oracle check."""
     import tempfile
     from ix_amd import traces
     if not os.path.exists(LOOP_EXE):
@@ -739,34 +743,32 @@ def host_path(seconds: float = 3.0, threads=(1, 4, 16)):
     for direct in (0, 1):
         res["async_latency"]["direct" if direct else "copy"] = _loop_run(fpath, "async1", 120, n=64, seconds=1.0,
                                                                          direct=direct)
-    dump = os.path.join(tmp, "dump.bin")
-    recs = None
-    for t in threads:
-        kw = dict(threads=t, seconds=seconds, batch=64, arena=1 << 17)
-        if t == threads[0]:
+    checks = []
+
+    def loop(path, name, tr, dump_name=None, **kw):
+        dump = os.path.join(tmp, dump_name) if dump_name else None
+        if dump:
             kw["dump"] = dump
-        res["loop"][f"threads{t}"] = _loop_run(fpath, "loop", 300, **kw)
-        if t == threads[0] and os.path.exists(dump):
-            recs = np.fromfile(dump, dtype=np.uint8).reshape(-1, 16)
-    # zero copy: the mbuf arenas registered, the kernels read the frames in
-    # place over the host link (ixg_rx_register_memory)
-    dump_zc = os.path.join(tmp, "dump_zc.bin")
+        res["loop"][name] = _loop_run(path, "loop", 300, seconds=seconds, batch=64, **kw)
+        if dump:
+            recs = np.fromfile(dump, dtype=np.uint8).reshape(-1, 16) if os.path.exists(dump) else None
+            if recs is not None and recs.shape[0] == tr.n:
+                checks.append(("hostpath", tr, recs, "hostpath_" + name))
+            else:
+                res["parity"] = "MISMATCH (no records dumped)"
+
     for t in threads:
-        kw = dict(threads=t, seconds=seconds, batch=64, arena=1 << 17, register=1)
-        if t == threads[0]:
-            kw["dump"] = dump_zc
-        res["loop"][f"threads{t}_zero_copy"] = _loop_run(fpath, "loop", 300, **kw)
-    if recs is not None and os.path.exists(dump_zc):
-        zc = np.fromfile(dump_zc, dtype=np.uint8).reshape(-1, 16)
-        if not np.array_equal(zc, recs):
-            recs = None  # the two passes must agree (and then both match the oracle)
-    if recs is not None and recs.shape[0] == pool.n:
-        check = ("hostpath", pool, recs)
-        res["parity"] = "pending oracle"
-    else:
-        check = None
-        res["parity"] = "MISMATCH (no records dumped)"
-    return res, check
+        loop(fpath, f"threads{t}", pool, "dump.bin" if t == threads[0] else None, threads=t, arena=1 << 17)
+    # 1514-B frames at the largest thread count: gathered, and read in place
+    # from the registered mbuf arenas over the host link
+    big = traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001)
+    bpath = os.path.join(tmp, "frames1514.bin")
+    write_frames_file(big, bpath)
+    t = threads[-1]
+    loop(bpath, f"tcp1514_threads{t}", big, None, threads=t, arena=1 << 15)
+    loop(bpath, f"tcp1514_threads{t}_zero_copy", big, "dump_zc.bin", threads=t, arena=1 << 15, register=1)
+    res.setdefault("parity", "pending oracle")
+    return res, checks
 
 
 def xgmi_leg(wl, eng, dist, world: int, rank: int, reps: int = 3):
@@ -963,6 +965,9 @@ def summary(res: dict) -> dict:
     if "loop" in hp:
         lp = hp["loop"]
         out["host_path"] = {k.replace("threads", "t"): lp[k].get("mpps") for k in lp}
+        top = max((k for k in lp if k.startswith("threads") and k[7:].isdigit()), key=lambda k: int(k[7:]), default=None)
+        if top:
+            out["host_path"]["t%s_max_latency_us" % top[7:]] = lp[top].get("latency_us", {}).get("max")
         out["host_path"]["parity"] = hp.get("parity")
     if "cpu_baseline" in res:
         out["cpu_baseline_mpps"] = res["cpu_baseline"]["value"]
@@ -1178,8 +1183,7 @@ def main():
         checks.append(mchk)
     if rank == 0 and world == 1 and not args.no_copy and args.workload == "c2":
         res["host_path"], hchk = host_path(seconds=args.host_seconds)
-        if hchk:
-            checks.append(hchk)
+        checks.extend(hchk)
     if rank == 0 and world == 1 and not args.no_copy:
         del wl
         torch.cuda.empty_cache()
@@ -1213,8 +1217,9 @@ def main():
                 if name in res["demux"]:
                     res["demux"][name]["parity"] = par["demux_" + name]
                     res["demux"][name]["kinds"] = par["demux_" + name + "_kinds"]
-        if "host_path" in res and "hostpath" in par:
-            res["host_path"]["parity"] = par["hostpath"]
+        if "host_path" in res and res["host_path"].get("parity") == "pending oracle":
+            hp = [v for k, v in par.items() if k.startswith("hostpath_")]
+            res["host_path"]["parity"] = "ok" if hp and all(v == "ok" for v in hp) else "MISMATCH"
         if "mbuf_path" in res:
             res["mbuf_path"]["parity"] = par["mbufs"] if res["mbuf_path"]["parity"] != "MISMATCH" else "MISMATCH"
         for kind in res.get("tx", {}):
