@@ -81,7 +81,7 @@ struct ixg_ctx {
 	/* PCB demux tables (ixg_demux_load) */
 	int demux_loaded;
 	uint32_t dmx_nfg, dmx_nout, dmx_nlisten;
-	uint32_t *d_astart, *d_twstart;
+	uint32_t *d_astart;
 	struct ixg_pcb_key *d_active, *d_tw;
 	struct ixg_listen_key *d_listen;
 	uint32_t *d_bline;           /* nfg*512 bucket lines of 64 B (ixgrx_walk.h) */

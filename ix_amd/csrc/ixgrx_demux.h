@@ -20,7 +20,6 @@ struct ixg_dparams {
 	const uint32_t *active_start; /* nfg*512 + 1 */
 	const uint32_t *bline;        /* nfg*512 bucket lines (ixgrx_walk.h) */
 	const struct ixg_pcb_key *active;
-	const uint32_t *tw_start;     /* nfg + 1 */
 	const struct ixg_pcb_key *tw;
 	const struct ixg_listen_key *listen;
 	uint32_t stride;

@@ -100,7 +100,7 @@ DEV void prep_item(const DParams& p, uint32_t i, int lane, const Item& it, Pend&
 }
 
 DEV ixgwalk::Tables tables(const DParams& p) {
-  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
+  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
 }
 
 // match chunk c's pending lookups (buf: the wave's 4 KiB of LDS); the ones

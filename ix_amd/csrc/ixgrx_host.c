@@ -144,7 +144,6 @@ void ixg_rx_fini(void *vctx)
 	hipFree(c->d_out);
 	hipFree(c->d_csum);
 	hipFree(c->d_astart);
-	hipFree(c->d_twstart);
 	hipFree(c->d_active);
 	hipFree(c->d_tw);
 	hipFree(c->d_listen);
@@ -269,7 +268,6 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		p.active_start = c->d_astart;
 		p.bline = c->d_bline;
 		p.active = c->d_active;
-		p.tw_start = c->d_twstart;
 		p.tw = c->d_tw;
 		p.listen = c->d_listen;
 		p.nfg = c->dmx_nfg;
@@ -836,6 +834,23 @@ static int upload(void **dst, const void *src, size_t bytes)
 	return 0;
 }
 
+/* tcp_to_idx of a pcb (inc/lwip/lwip/tcp_impl.h:371-387): the crc32q stream
+ * of local ip, remote ip and (int)(local_port << 16 | remote_port), as the
+ * kernels compute it from a segment's tuple through the byte tables
+ * (ixg_rx_hash_tables: k_crc_pos) */
+static uint32_t pcb_bucket_of(const struct ixg_pcb_key *k)
+{
+	uint8_t s[24];
+	memset(s, 0, sizeof(s));
+	memcpy(s, &k->local_ip, 4);
+	memcpy(s + 8, &k->remote_ip, 4);
+	const uint32_t ports = (uint32_t)k->remote_port | ((uint32_t)k->local_port << 16);
+	memcpy(s + 16, &ports, 4);
+	if (ports & 0x80000000u)
+		memset(s + 20, 0xff, 4);
+	return crc_stream(IXG_PCB_HASH_SEED, s) & (IXG_PCB_BUCKETS - 1u);
+}
+
 static int csr_ok(const uint32_t *start, size_t rows)
 {
 	if (!start || start[0] != 0)
@@ -863,16 +878,23 @@ int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
 	c->demux_loaded = 0;
 	int rc;
 	if ((rc = upload((void **)&c->d_astart, t->active_start, (na_rows + 1) * sizeof(uint32_t))) ||
-	    (rc = upload((void **)&c->d_twstart, t->tw_start, (ng + 1) * sizeof(uint32_t))) ||
 	    (rc = upload((void **)&c->d_active, t->active, na * sizeof(struct ixg_pcb_key))) ||
-	    (rc = upload((void **)&c->d_tw, t->tw, ntw * sizeof(struct ixg_pcb_key))) ||
 	    (rc = upload((void **)&c->d_listen, t->listen, (size_t)t->n_listen * sizeof(struct ixg_listen_key))))
 		return rc;
-	/* the bucket lines (ixgrx_walk.h): count, CSR start, the first
-	 * IXG_BUCKET_INLINE entries of each active list, in list order */
+	/* the bucket lines (ixgrx_walk.h): count, CSR start, the bucket's
+	 * TIME-WAIT run (count, start), the first 3 entries of each active list,
+	 * in list order */
 	uint32_t *bl = (uint32_t *)calloc(na_rows ? na_rows : 1, 64);
-	if (!bl)
+	/* each group's TIME-WAIT list split into per-bucket runs, list order kept
+	 * within a run (a counting sort by row = group * 512 + bucket) */
+	uint32_t *twrow = (uint32_t *)malloc((ntw ? ntw : 1) * sizeof(uint32_t));
+	struct ixg_pcb_key *tw2 = (struct ixg_pcb_key *)malloc((ntw ? ntw : 1) * sizeof(struct ixg_pcb_key));
+	if (!bl || !twrow || !tw2) {
+		free(bl);
+		free(twrow);
+		free(tw2);
 		return -ENOMEM;
+	}
 	for (size_t r = 0; r < na_rows; r++) {
 		const uint32_t s0 = t->active_start[r], cnt = t->active_start[r + 1] - s0;
 		uint32_t *row = bl + 16 * r;
@@ -881,8 +903,27 @@ int ixg_demux_load(void *vctx, const struct ixg_demux_tables *t)
 		for (uint32_t k = 0; k < cnt && k < 3; k++)
 			memcpy(row + 4 + 4 * k, &t->active[s0 + k], sizeof(struct ixg_pcb_key));
 	}
+	for (size_t g = 0; g < ng; g++)
+		for (uint32_t k = t->tw_start[g]; k < t->tw_start[g + 1]; k++) {
+			twrow[k] = (uint32_t)(g * IXG_PCB_BUCKETS) + pcb_bucket_of(&t->tw[k]);
+			bl[16 * (size_t)twrow[k] + 2]++;
+		}
+	uint32_t run = 0;
+	for (size_t r = 0; r < na_rows; r++) {
+		bl[16 * r + 3] = run;
+		run += bl[16 * r + 2];
+		bl[16 * r + 2] = 0; /* refilled as the entries are placed */
+	}
+	for (size_t k = 0; k < ntw; k++) {
+		uint32_t *row = bl + 16 * (size_t)twrow[k];
+		tw2[row[3] + row[2]++] = t->tw[k];
+	}
 	rc = upload((void **)&c->d_bline, bl, na_rows * 64);
+	if (!rc)
+		rc = upload((void **)&c->d_tw, tw2, ntw * sizeof(struct ixg_pcb_key));
 	free(bl);
+	free(twrow);
+	free(tw2);
 	if (rc)
 		return rc;
 	c->dmx_nfg = t->nfg;
@@ -904,7 +945,6 @@ static int demux_launch(struct ixg_ctx *c, const uint8_t *base, const uint64_t *
 	p.active_start = c->d_astart;
 	p.bline = c->d_bline;
 	p.active = c->d_active;
-	p.tw_start = c->d_twstart;
 	p.tw = c->d_tw;
 	p.listen = c->d_listen;
 	p.stride = stride;

@@ -47,7 +47,6 @@ struct ixg_kparams {
 	const uint32_t *active_start;
 	const uint32_t *bline;        /* nfg*512 bucket lines (ixgrx_walk.h) */
 	const struct ixg_pcb_key *active;
-	const uint32_t *tw_start;
 	const struct ixg_pcb_key *tw;
 	const struct ixg_listen_key *listen;
 	uint32_t nfg;          /* the snapshot's local flow groups */

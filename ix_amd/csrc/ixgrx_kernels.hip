@@ -640,7 +640,7 @@ DEV void store_demux(const KParams& p, uint32_t i, const Rec& r, uint32_t src, u
   if (!DMX || !p.dmx) return;
   uint32_t id = 0, kind = IXG_D_NONE;
   if (((r.w0 >> 16) & 0xffu) == IXG_V_TCP) {
-    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
+    const ixgwalk::Tables t{p.active_start, p.bline, p.active, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
     ixgwalk::walk(t, ixg_demux_group(r.w0 & 0xffffu, p.fg_base, p.nfg, p.n_out), r.w3 & 0xffffu, (r.w3 >> 16) & 0xffu,
                   src, dst, ports, id, kind);
   }
@@ -1601,7 +1601,7 @@ struct PendDmx {
 constexpr uint32_t kNoDmx = 0xffffffffu;
 
 DEV ixgwalk::Tables dmx_tables(const KParams& p) {
-  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw_start, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
+  return ixgwalk::Tables{p.active_start, p.bline, p.active, p.tw, p.listen, p.nfg + p.n_out, p.n_listen};
 }
 
 // record r of frame i of chunk c (valid lanes) -> pending lookup, the

@@ -16,12 +16,16 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // The list snapshot of ixg_demux_load, in HBM (small; L2 / Infinity Cache).
 struct Tables {
   const uint32_t* active_start;  // nfg*512 + 1
-  // per active bucket one 64-byte line: {count, CSR start, 0, 0} + the first
-  // three entries of the list in list order, so the common case (a short
-  // bucket) is ONE dependent load instead of bounds then entries
+  // per active bucket one 64-byte line: {count, CSR start, TIME-WAIT count,
+  // TIME-WAIT start} + the first three entries of the active list in list
+  // order, so the common case (a short bucket) is ONE dependent load instead
+  // of bounds then entries
   const uint32_t* bline;
   const ixg_pcb_key* active;
-  const uint32_t* tw_start;      // nfg + 1
+  // each group's TIME-WAIT list split into per-bucket runs in list order
+  // (ixg_demux_load): a segment can only match a pcb of its own 4-tuple,
+  // whose tcp_to_idx bucket is the segment's, so the first match in the
+  // bucket's run is the first match in the group's list
   const ixg_pcb_key* tw;
   const ixg_listen_key* listen;
   uint32_t nfg;  // groups in the snapshot: local, then outbound (ixg_demux_group)
@@ -104,8 +108,8 @@ __device__ __forceinline__ void lines_exchange(const u32x4 (&piece)[4], int lane
 // TIME-WAIT list, then the listen list or the reset / drop verdict. fg not a
 // group of the tables: straight to the listen list.
 __device__ __forceinline__ void walk_rest(const Tables& t, uint32_t fg, uint32_t tflags, uint32_t src, uint32_t dst,
-                                          uint32_t ports, uint32_t start, uint32_t cnt, uint32_t& id,
-                                          uint32_t& kind) {
+                                          uint32_t ports, const u32x4& hd, uint32_t& id, uint32_t& kind) {
+  const uint32_t start = hd.y, cnt = hd.x;
   bool hit = false;
   id = 0;
   kind = IXG_D_NONE;
@@ -113,7 +117,7 @@ __device__ __forceinline__ void walk_rest(const Tables& t, uint32_t fg, uint32_t
     if (cnt > 3u) hit = find_list(t.active, start + 3u, start + cnt, ports, src, dst, id);
     if (hit) {
       kind = IXG_D_ACTIVE;  // tcp_in.c:249-256
-    } else if (find_list(t.tw, t.tw_start[fg], t.tw_start[fg + 1], ports, src, dst, id)) {
+    } else if (hd.z && find_list(t.tw, hd.w, hd.w + hd.z, ports, src, dst, id)) {
       kind = IXG_D_TIMEWAIT;  // tcp_in.c:260-269
       hit = true;
     }
@@ -181,14 +185,10 @@ __device__ __forceinline__ void slowq_flush(const Tables& t, SlowQ& q, int lane,
       ports = (((sp & 0xffu) << 8) | (sp >> 8)) | ((((dp & 0xffu) << 8) | (dp >> 8)) << 16);
     }
     const uint32_t g = q.key & 0x3fffu;
-    uint32_t start = 0, cnt = 0;
-    if (g < t.nfg) {
-      const u32x4 hd = reinterpret_cast<const u32x4*>(t.bline)[4u * (g * IXG_PCB_BUCKETS + ((q.key >> 14) & 0x1ffu))];
-      start = hd.y;
-      cnt = hd.x;
-    }
+    u32x4 hd = u32x4{0u, 0u, 0u, 0u};
+    if (g < t.nfg) hd = reinterpret_cast<const u32x4*>(t.bline)[4u * (g * IXG_PCB_BUCKETS + ((q.key >> 14) & 0x1ffu))];
     uint32_t id, kind;
-    walk_rest(t, g, q.key >> 23, src, dst, ports, start, cnt, id, kind);
+    walk_rest(t, g, q.key >> 23, src, dst, ports, hd, id, kind);
     typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
     reinterpret_cast<u32x2v*>(out)[q.i] = u32x2v{id, kind};
   }
@@ -280,7 +280,7 @@ __device__ __forceinline__ void walk(const Tables& t, uint32_t fg, uint32_t buck
     }
     if (hit) {
       kind = IXG_D_ACTIVE;  // tcp_in.c:249-256
-    } else if (find_list(t.tw, t.tw_start[fg], t.tw_start[fg + 1], ports, src, dst, id)) {
+    } else if (hd.z && find_list(t.tw, hd.w, hd.w + hd.z, ports, src, dst, id)) {
       kind = IXG_D_TIMEWAIT;  // tcp_in.c:260-269
       hit = true;
     }
