@@ -388,6 +388,22 @@ struct ixg_tcp_ext {
 int ixg_tcp_ext_batch_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec,
 			  uint32_t n, struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream);
 
+/* ---- ICMP echo reflect ---------------------------------------------------- */
+
+/* For every frame whose record is IXG_V_ICMP_ECHO, rewrite the frame in place
+ * into the echo reply icmp_input leaves in the mbuf for eth_send_one
+ * (dp/net/icmp.c:44-71,88-91): ICMP type ICMP_ECHOREPLY; Ethernet destination
+ * = the old source, source = mac (CFG.mac); IP destination = the old source,
+ * source = hton32(host_addr) (CFG.host_addr, host order as IX's cfg holds
+ * it); the ICMP checksum = chksum_internet over the record's l4_len bytes.
+ * As in the reference, the IP header checksum is left as it was (the reply
+ * goes out with ol_flags 0): it stays valid when host_addr is the request's
+ * destination. Other frames are untouched. Device-resident frames (any
+ * alignment) and the records ixg_rx_batch_dev produced for them (8-byte
+ * aligned); asynchronous on `stream`. 0 or -errno. */
+int ixg_icmp_reflect_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec, uint32_t n,
+			 const uint8_t mac[6], uint32_t host_addr, void *stream);
+
 /* ---- PCB demux: the tcp_input step after the head ---- */
 
 /* For each IXG_V_TCP record, find the PCB the segment belongs to, exactly as

@@ -14,6 +14,7 @@
 #include "ixgrx_tcpx.h"
 #include "ixgrx_tx.h"
 #include "ixgrx_ev.h"
+#include "ixgrx_icmp.h"
 
 /* ---- hash tables -------------------------------------------------------- */
 
@@ -1016,6 +1017,28 @@ int ixg_tcp_ext_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const stru
 	p.n = n;
 	p.flags = flags;
 	return ixgrx_tcpx_launch(&p, stream) == 0 ? 0 : -EIO;
+}
+
+int ixg_icmp_reflect_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec, uint32_t n,
+			 const uint8_t mac[6], uint32_t host_addr, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || !mac || (n && (!fr->base || !d_rec)) || ((uintptr_t)d_rec & 7) || ((uintptr_t)fr->off & 7))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	HIPCHK(hipSetDevice(c->device));
+	struct ixg_iparams p;
+	memset(&p, 0, sizeof(p));
+	p.base = (uint8_t *)(uintptr_t)fr->base;
+	p.off = fr->off;
+	p.rec = d_rec;
+	p.stride = fr->stride;
+	p.n = n;
+	memcpy(p.mac, mac, 6);
+	const uint32_t be = __builtin_bswap32(host_addr); /* hton32 (icmp.c:55) */
+	memcpy(p.host, &be, 4);
+	return ixgrx_icmp_launch(&p, stream) == 0 ? 0 : -EIO;
 }
 
 int ixg_demux_batch_host(void *vctx, const void *frames, const uint64_t *off, const uint16_t *len, uint32_t stride,

@@ -1,0 +1,127 @@
+// ixgrx_icmp.hip - MI355X (gfx950) kernel for ICMP echo reflect
+// (dp/net/icmp.c:44-71,88-91): every frame whose record is IXG_V_ICMP_ECHO
+// becomes its echo reply in place, as icmp_input leaves it in the mbuf for
+// eth_send_one: ICMP type 0; Ethernet destination = the old source, source
+// = CFG.mac; IP destination = the old source, source = hton32(CFG.host_addr)
+// (the IP checksum is not recomputed: the reference sends with ol_flags 0);
+// the ICMP checksum = chksum_internet over the message with type and
+// checksum zero.
+//
+// One wave per 64 records. The record reads are the kernel's traffic when
+// echo requests are rare (IX's case); the wave then takes its echo frames one
+// at a time: all 64 lanes sum the message's dwords (a 1472-byte ping is 6
+// dwords per lane), a cross-lane one's-complement reduction gives the
+// checksum, and 23 lanes write one rewritten header byte each (frames of any
+// alignment). A frame whose message starts at an odd address sums byte-
+// swapped 16-bit words: the folded sum is swapped back (RFC 1071 byte-order
+// independence).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ixgrx.h"
+#include "ixgrx_icmp.h"
+
+#define DEV __device__ __forceinline__
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+DEV uint32_t add1c(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s + (s < a ? 1u : 0u);
+}
+
+DEV uint32_t fold16(uint32_t s) {
+  s = (s & 0xffffu) + (s >> 16);
+  return (s & 0xffffu) + (s >> 16);
+}
+
+template <bool OFFS>
+DEV void reflect(const ixg_iparams& p) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t c = (uint64_t)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  const uint64_t i = c * 64u + (uint64_t)lane;
+  bool echo = false;
+  uint32_t meta = 0;  // l4_off | l4_len << 16
+  if (i < p.n) {
+    const u32x2 r = reinterpret_cast<const u32x2*>(p.rec)[2u * i];
+    echo = ((r.x >> 16) & 0xffu) == IXG_V_ICMP_ECHO;
+    meta = r.y;
+  }
+  for (uint64_t m = __builtin_amdgcn_ballot_w64(echo); m; m &= m - 1u) {
+    const int e = __builtin_ctzll(m);
+    const uint64_t fi = c * 64u + (uint64_t)e;
+    const uint32_t fm = __builtin_amdgcn_readlane(meta, e);
+    const uint32_t off = fm & 0xffffu, len = fm >> 16;  // icmp_input's len >= 8
+    uint8_t* f = p.base + (OFFS ? p.off[fi] : fi * (uint64_t)p.stride);
+    // the message [a, a + len) as aligned dwords; byte k of dword j is
+    // message byte 4j + k - s
+    const uintptr_t a = reinterpret_cast<uintptr_t>(f) + off;
+    const uint32_t s = (uint32_t)(a & 3u);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a - s);
+    const uint32_t nd = (s + len + 3u) >> 2;
+    uint32_t acc = 0;
+    for (uint32_t j = (uint32_t)lane; j < nd; j += 64u) {
+      uint32_t v = w[j];
+      if (j == 0u || j == 1u || j + 1u == nd) {
+        // keep message bytes 1 (code) and 4 .. len-1: the type (0) and the
+        // checksum field (2, 3) count as zero
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          const int t = (int)(4u * j) + k - (int)s;
+          const bool keep = t == 1 || (t >= 4 && t < (int)len);
+          if (!keep) v &= ~(0xffu << (8 * k));
+        }
+      }
+      acc = add1c(acc, v);
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc = add1c(acc, (uint32_t)__shfl_xor((int)acc, d, 64));
+    uint32_t sum = fold16(acc);
+    if (s & 1u) sum = ((sum & 0xffu) << 8) | (sum >> 8);
+    const uint32_t ck = (~sum) & 0xffffu;  // chksum_internet, stored as is
+    // the header bytes, one lane each: Ethernet dhost = shost, shost =
+    // CFG.mac (icmp.c:50-51); IP dst = src, src = CFG.host_addr (:54-55);
+    // type = ICMP_ECHOREPLY (:89), checksum (:57-58)
+    if (lane < 23) {
+      uint32_t at, val;
+      if (lane < 6) {
+        at = (uint32_t)lane;
+        val = f[6 + lane];
+      } else if (lane < 12) {
+        at = (uint32_t)lane;
+        val = p.mac[lane - 6];
+      } else if (lane < 16) {
+        at = 30u + (uint32_t)(lane - 12);
+        val = f[26 + (lane - 12)];
+      } else if (lane < 20) {
+        at = 26u + (uint32_t)(lane - 16);
+        val = p.host[lane - 16];
+      } else if (lane == 20) {
+        at = off;
+        val = 0u;
+      } else {
+        at = off + 2u + (uint32_t)(lane - 21);
+        val = lane == 21 ? (ck & 0xffu) : (ck >> 8);
+      }
+      f[at] = (uint8_t)val;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_icmp_reflect_s(ixg_iparams p) { reflect<false>(p); }
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_icmp_reflect_o(ixg_iparams p) { reflect<true>(p); }
+
+extern "C" int ixgrx_icmp_launch(const void* params, void* stream) {
+  const ixg_iparams& p = *static_cast<const ixg_iparams*>(params);
+  const uint64_t grid = ((uint64_t)p.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(p.off ? ixg_icmp_reflect_o : ixg_icmp_reflect_s, dim3((uint32_t)grid), dim3(kBlock), 0,
+                     (hipStream_t)stream, p);
+  return (int)hipGetLastError();
+}

@@ -135,6 +135,34 @@ def build_ipv4(rng: np.random.Generator, n: int, L: int, proto: int, ihl: int = 
     return f
 
 
+def icmp_echo(rng: np.random.Generator, payload: int, ihl: int = 5) -> bytes:
+    """One ICMP echo request (type 8) with `payload` random bytes after the
+    8-byte header, valid IP and ICMP checksums, padded to the 60-byte
+    Ethernet minimum."""
+    l4 = 14 + 4 * ihl
+    ip_len = 4 * ihl + 8 + payload
+    f = np.zeros((1, max(60, 14 + ip_len)), dtype=np.uint8)
+    f[0, 0:6] = [0x02, 0, 0, 0, 0, 0x01]
+    f[0, 6:12] = rng.integers(0, 256, 6, dtype=np.uint8)
+    f[0, 12] = 0x08
+    f[0, 14] = 0x40 | ihl
+    _put16(f, 16, np.array([ip_len]))
+    _put16(f, 18, rng.integers(0, 65536, 1))
+    f[0, 22] = 64
+    f[0, 23] = 1
+    f[0, 26:34] = rng.integers(0, 256, 8, dtype=np.uint8)
+    if ihl > 5:
+        f[0, 34:l4] = 0x01
+    f[0, l4] = 8
+    f[0, l4 + 4:l4 + 8 + payload] = rng.integers(0, 256, 4 + payload, dtype=np.uint8)
+    _put16(f, 24, (~_fold(_sum_be16(f[:, 14:l4]))) & 0xFFFF)
+    seg = f[:, l4:14 + ip_len]
+    if seg.shape[1] % 2:
+        seg = np.concatenate([seg, np.zeros((1, 1), np.uint8)], axis=1)
+    _put16(f, l4 + 2, (~_fold(_sum_be16(seg))) & 0xFFFF)
+    return f[0].tobytes()
+
+
 def build_ipv6(rng: np.random.Generator, n: int, L: int, proto: int) -> np.ndarray:
     """Ethernet + IPv6 (no extension headers) + TCP/UDP, valid checksums."""
     hl = 20 if proto == 6 else 8

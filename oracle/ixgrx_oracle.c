@@ -738,6 +738,38 @@ int ixgo_demux_batch(const struct ixg_demux_tables *t, uint32_t fg_base, const u
 	return 0;
 }
 
+/* ---- ICMP echo reflect (dp/net/icmp.c:44-71,88-91) -------------------------- */
+
+/* For every frame whose record is IXG_V_ICMP_ECHO, what icmp_input's
+ * ICMP_ECHO case leaves in the mbuf: hdr->type = ICMP_ECHOREPLY (:89), then
+ * icmp_reflect (:44-71): Ethernet dhost = shost, shost = CFG.mac; IP dst =
+ * src, src = hton32(CFG.host_addr) (the IP checksum is not recomputed: the
+ * frame leaves with ol_flags 0); hdr->chksum = 0 then chksum_internet over
+ * the ICMP length (the record's l4_len, ip_input's len). Returns the number
+ * of frames rewritten. */
+uint32_t ixgo_icmp_reflect_batch(uint8_t *base, const uint64_t *off, uint32_t stride, const struct ixg_rx_rec *rec,
+				 uint32_t n, const uint8_t mac[6], uint32_t host_addr)
+{
+	uint32_t k = 0;
+	for (uint32_t i = 0; i < n; i++) {
+		if (rec[i].verdict != IXG_V_ICMP_ECHO)
+			continue;
+		uint8_t *f = base + (off ? off[i] : (uint64_t)i * stride);
+		uint8_t *h = f + rec[i].l4_off;
+		h[0] = 0; /* ICMP_ECHOREPLY */
+		memmove(f, f + 6, 6);
+		memcpy(f + 6, mac, 6);
+		memmove(f + 30, f + 26, 4);
+		const uint32_t be = __builtin_bswap32(host_addr);
+		memcpy(f + 26, &be, 4);
+		h[2] = h[3] = 0;
+		const uint16_t c = ixgo_chksum_internet(h, rec[i].l4_len);
+		memcpy(h + 2, &c, 2);
+		k++;
+	}
+	return k;
+}
+
 /* ---- TX: header build + checksums ------------------------ */
 
 /* ---- the rest of the tcp_input head (tcp_in.c:230-241) --------------------- */

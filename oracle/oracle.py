@@ -62,6 +62,8 @@ def lib() -> ctypes.CDLL:
         L.ixgo_ev_batch.restype = u32
         L.ixgo_tcp_ext_batch.argtypes = [vp, vp, u32, vp, u32, u32, vp]
         L.ixgo_tcp_ext_batch.restype = i32
+        L.ixgo_icmp_reflect_batch.argtypes = [vp, vp, u32, vp, u32, vp, u32]
+        L.ixgo_icmp_reflect_batch.restype = u32
         _lib = L
     return _lib
 
@@ -259,6 +261,20 @@ def ev_batch(blob: np.ndarray, off, stride: int, rec: np.ndarray, dmx, pcbs, iom
 
 TCPX_DTYPE = np.dtype([("seqno", "<u4"), ("ackno", "<u4"), ("wnd", "<u2"), ("tcplen", "<u2"),
                        ("src_port", "<u2"), ("dst_port", "<u2")])
+
+
+def icmp_reflect_batch(blob: np.ndarray, off, stride: int, rec: np.ndarray, mac: bytes, host_addr: int):
+    """ICMP echo reflect (oracle/ixgrx_oracle.c ixgo_icmp_reflect_batch):
+    (the frames with every IXG_V_ICMP_ECHO one rewritten, the count)."""
+    L = lib()
+    b = np.ascontiguousarray(blob, dtype=np.uint8).copy()
+    n = int(rec.shape[0])
+    offa = None if off is None else np.ascontiguousarray(off, dtype=np.uint64)
+    r = np.ascontiguousarray(rec).view(np.uint8).reshape(n, 16)
+    m = (ctypes.c_uint8 * 6).from_buffer_copy(bytes(mac))
+    k = L.ixgo_icmp_reflect_batch(b.ctypes.data, None if offa is None else offa.ctypes.data, stride, r.ctypes.data,
+                                  n, m, host_addr)
+    return b, int(k)
 
 
 def tcp_ext_batch(blob: np.ndarray, off, stride: int, rec: np.ndarray, flags: int = 0):

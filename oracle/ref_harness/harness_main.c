@@ -28,14 +28,19 @@
  * Input file  (LE): "IXGRXIN1", u32 n, u32 cfg_flags, u16 nb_rx_fgs, u16 dev_idx,
  *                   u8 key[40], u16 len[n], u32 off[n], u32 blob_len, blob,
  *                   optionally "FDIR", u32 nf, u16 cpu_id, u16 0,
- *                   struct ixg_fdir_filter[nf].
+ *                   struct ixg_fdir_filter[nf], and/or "HOST", u8 mac[6],
+ *                   u16 0, u32 host_addr (CFG.mac / CFG.host_addr for
+ *                   icmp_reflect; host order).
  * Output file (LE): "IXGRXOUT", u32 n, struct ixg_rx_rec[n] (16 B), u32 csum[n],
  *                   u8 confirm[n] (0: eth_input did not drop the frame; 1: it
  *                   did and confirm_drop pinned the reason; 2: not pinned),
  *                   "TCPX", struct ixg_tcp_ext[n], u8 hdr[n][16] (the rest of
  *                   the tcp_input head from the reference's own tcp_input,
  *                   ref_tcphead.c: its LWIP_Context fields and the segment's
- *                   first 16 bytes as it converted them in place).
+ *                   first 16 bytes as it converted them in place),
+ *                   "ICMP", u8 reflected[n], then each frame as eth_input left
+ *                   it in its mbuf (len[i] bytes each: icmp_reflect rewrote
+ *                   the ICMP_ECHO ones in place, dp/net/icmp.c:44-71).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -206,6 +211,9 @@ static unsigned int fdir_cpu;
  * them (converted to host order in place); zero for every other verdict */
 static struct ixg_tcp_ext th_ext;
 static uint8_t th_hdr[16];
+/* the frame as eth_input left it (icmp_reflect rewrites echo requests) */
+static uint8_t after[IXG_MBUF_DATA_LEN];
+static uint8_t reflected;
 
 static uint16_t h16(const uint8_t *p)
 {
@@ -257,6 +265,8 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 	memset(r, 0, sizeof(*r));
 	memset(&th_ext, 0, sizeof(th_ext));
 	memset(th_hdr, 0, sizeof(th_hdr));
+	memcpy(after, frame, L);
+	reflected = 0;
 	*confirm = 0;
 	r->pcb_bucket = IXG_NO_BUCKET;
 	memset(f, 0, sizeof(f));
@@ -448,6 +458,8 @@ static void one(const struct ixg_rx_cfg *cfg, const uint8_t *frame, uint32_t L, 
 		r->l4_len = (uint16_t)(L >= 14 ? L - 14 : 0);
 		return;
 	case REF_ICMP_REFLECT:
+		memcpy(after, mbuf + IXG_MBUF_HEADER_LEN, L);
+		reflected = 1;
 		r->verdict = IXG_V_ICMP_ECHO;
 		r->l4_off = (uint16_t)l4;
 		r->l4_len = (uint16_t)(ip_len - ihl * 4);
@@ -493,7 +505,17 @@ int main(int argc, char **argv)
 	if (fread(blob, 1, blob_len, fi) != blob_len)
 		die("short blob", 0);
 	char tag[4];
-	if (fread(tag, 1, 4, fi) == 4 && !memcmp(tag, "FDIR", 4)) {
+	uint8_t host_mac[6] = {0};
+	uint32_t host_addr = 0;
+	while (fread(tag, 1, 4, fi) == 4) {
+		if (!memcmp(tag, "HOST", 4)) {
+			uint16_t pad;
+			if (fread(host_mac, 1, 6, fi) != 6 || fread(&pad, 2, 1, fi) != 1 || fread(&host_addr, 4, 1, fi) != 1)
+				die("short host block", 0);
+			continue;
+		}
+		if (memcmp(tag, "FDIR", 4))
+			die("unknown input block", 0);
 		uint16_t cpu, pad;
 		if (fread(&n_fdir, 4, 1, fi) != 1 || fread(&cpu, 2, 1, fi) != 1 || fread(&pad, 2, 1, fi) != 1)
 			die("short fdir header", 0);
@@ -507,18 +529,23 @@ int main(int argc, char **argv)
 
 	if (ref_ix_init())
 		die("arch_prctl(ARCH_SET_GS)", 0);
+	ref_set_host(host_mac, host_addr);
 	uint8_t *mbuf = aligned_alloc(64, IXG_MBUF_STRIDE);
 	struct ixg_rx_rec *recs = calloc(n + 1, sizeof(*recs));
 	uint32_t *cs = calloc(n + 1, sizeof(*cs));
 	uint8_t *cf = calloc(n + 1, 1);
 	struct ixg_tcp_ext *ext = calloc(n + 1, sizeof(*ext));
 	uint8_t *hdr = calloc(n + 1, 16);
+	uint8_t *refl = calloc(n + 1, 1);
+	uint8_t *outb = malloc(blob_len + 1);
 	for (uint32_t i = 0; i < n; i++) {
 		if (len[i] > IXG_MBUF_DATA_LEN || (uint64_t)off[i] + len[i] > blob_len)
 			die("frame does not fit an mbuf", i);
 		one(&cfg, blob + off[i], len[i], mbuf, &recs[i], &cs[i], &cf[i], i);
 		ext[i] = th_ext;
 		memcpy(hdr + 16 * (size_t)i, th_hdr, 16);
+		refl[i] = reflected;
+		memcpy(outb + off[i], after, len[i]);
 	}
 	FILE *fo = fopen(argv[2], "wb");
 	if (!fo)
@@ -531,6 +558,10 @@ int main(int argc, char **argv)
 	fwrite("TCPX", 1, 4, fo);
 	fwrite(ext, sizeof(*ext), n, fo);
 	fwrite(hdr, 16, n, fo);
+	fwrite("ICMP", 1, 4, fo);
+	fwrite(refl, 1, n, fo);
+	for (uint32_t i = 0; i < n; i++)
+		fwrite(outb + off[i], 1, len[i], fo);
 	fclose(fo);
 	if (tsec > 0 && n > 0) {
 		struct timespec t0, t1;

@@ -20,6 +20,7 @@ int ref_ix_init(void);
 uint32_t ref_fg_transition(uint32_t fg_id, unsigned int cpu);
 void ref_eth_input(void *mbuf);
 uint16_t ref_chksum_internet(const void *buf, int len);
+void ref_set_host(const uint8_t mac[6], uint32_t host_addr);
 
 uint16_t ref_pseudo_partial(const void *seg, uint16_t len, uint8_t proto, uint16_t proto_len,
 			    uint32_t src_raw, uint32_t dst_raw);

@@ -125,6 +125,14 @@ void ref_eth_input_raw(void *mbuf)
 	eth_input(NULL, (struct mbuf *)mbuf);
 }
 
+/* icmp_reflect's source MAC and IP address (CFG.mac, CFG.host_addr, host
+ * order as cfg.c stores it) */
+void ref_set_host(const uint8_t mac[6], uint32_t host_addr)
+{
+	memcpy(&CFG.mac, mac, 6);
+	CFG.host_addr.addr = host_addr;
+}
+
 uint16_t ref_chksum_internet(const void *buf, int len)
 {
 	return chksum_internet((const char *)buf, len);

@@ -384,6 +384,11 @@ int ixgrx_ev_launch(const void *p, uint32_t ncu, void *s)
 	(void)p; (void)ncu; (void)s;
 	return -1;
 }
+int ixgrx_icmp_launch(const void *p, void *s)
+{
+	(void)p; (void)s;
+	return -1;
+}
 int ixgrx_tcpx_launch(const void *p, void *s)
 {
 	(void)p; (void)s;

@@ -44,9 +44,11 @@ def fdir_filter(f: bytes, swap: bool = False) -> bytes:
 
 
 def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir: list[bytes] | None = None,
-            cpu: int = 0, full: bool = False):
+            cpu: int = 0, full: bool = False, host: tuple[bytes, int] | None = None):
     """(records, residuals) from the reference's eth_input; full: also the
-    rest of the tcp_input head from its tcp_input (tcpx, tcpx_hdr)."""
+    rest of the tcp_input head from its tcp_input (tcpx, tcpx_hdr); host =
+    (mac, host_addr): also (reflected flags, frames after eth_input) with
+    CFG.mac / CFG.host_addr set for icmp_reflect."""
     lens = np.array([len(f) for f in frames], dtype=np.uint16)
     offs = np.zeros(len(frames), dtype=np.uint32)
     if frames:
@@ -66,6 +68,8 @@ def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir
                 f.write(b"FDIR")
                 f.write(struct.pack("<IHH", len(fdir), cpu, 0))
                 f.write(b"".join(fdir))
+            if host:
+                f.write(b"HOST" + host[0] + b"\0\0" + struct.pack("<I", host[1]))
         subprocess.run([HARNESS, fi, fo], check=True)
         raw = open(fo, "rb").read()
     assert raw[:8] == b"IXGRXOUT"
@@ -89,6 +93,12 @@ def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir
     assert raw[o:o + 4] == b"TCPX"
     tcpx = np.frombuffer(raw, dtype=np.uint8, count=16 * n, offset=o + 4).reshape(n, 16).copy()
     tcpx_hdr = np.frombuffer(raw, dtype=np.uint8, count=16 * n, offset=o + 4 + 16 * n).reshape(n, 16).copy()
+    o += 4 + 32 * n
+    assert raw[o:o + 4] == b"ICMP"
+    refl = np.frombuffer(raw, dtype=np.uint8, count=n, offset=o + 4).copy()
+    after = np.frombuffer(raw, dtype=np.uint8, count=int(lens.astype(np.int64).sum()), offset=o + 4 + n).copy()
+    if host:
+        return rec, csum, refl, after
     return (rec, csum, tcpx, tcpx_hdr) if full else (rec, csum)
 
 
@@ -333,9 +343,70 @@ def save(name: str, frames: list[bytes], key: bytes, nb: int, dev: int, flags: i
     print(f"{name}: {len(frames)} frames, verdicts {dict(zip(*np.unique(v, return_counts=True)))}")
 
 
+def icmp_frames(rng: np.random.Generator) -> list[bytes]:
+    """Echo requests icmp_input reflects (every ICMP length class, odd and
+    even, IP options, Ethernet padding past the IP length, the largest mbuf
+    frame, host address equal to and different from the frame's
+    destination) among frames it does not (other ICMP types, bad checksum,
+    short) and non-ICMP frames."""
+    fr = []
+    for pl in list(range(0, 40)) + [55, 56, 64, 100, 255, 256, 511, 1000, 1472, 2048 - 42]:
+        fr.append(ipv4(proto=1, icmp_type=8, payload=bytes(rng.integers(0, 256, pl, dtype=np.uint8))))
+    for ihl in range(6, 16):
+        fr.append(ipv4(proto=1, icmp_type=8, ihl=ihl, payload=bytes(rng.integers(0, 256, 21, dtype=np.uint8))))
+        fr.append(ipv4(proto=1, icmp_type=8, ihl=ihl, payload=bytes(rng.integers(0, 256, 64, dtype=np.uint8))))
+    for L in (80, 128, 333):  # Ethernet padding past the IP length
+        fr.append(ipv4(proto=1, icmp_type=8, payload=b"pad", L=L))
+    for dst in (b"\x0a\x00\x00\x02", b"\xc0\xa8\x01\x07", b"\xff\xff\xff\xff"):
+        fr.append(ipv4(proto=1, icmp_type=8, dst=dst, payload=b"addr" * 3))
+    for t in (0, 3, 11, 13, 17):
+        fr.append(ipv4(proto=1, icmp_type=t, payload=b"other" * 3))
+    bad = bytearray(ipv4(proto=1, icmp_type=8, payload=b"bad checksum"))
+    bad[44] ^= 4
+    fr.append(bytes(bad))
+    fr.append(ipv4(proto=1, l4=b"\x08\x00\xf7\xff", fix_l4=False))
+    fr.append(ipv4(proto=6, payload=b"tcp"))
+    fr.append(ipv4(proto=17, payload=b"udp"))
+    return fr
+
+
+def save_icmp(key: bytes):
+    """icmp.npz: frames before and after the reference's eth_input with
+    CFG.mac / CFG.host_addr set (icmp_reflect rewrites ICMP_ECHO frames)."""
+    rng = np.random.default_rng(0x1B0009)
+    frames = icmp_frames(rng)
+    frames = frames + [bytes(f) for f in fuzz_frames(rng, 300) if len(f) > 23 and f[23] == 1]
+    mac = bytes([0x02, 0x1b, 0x0c, 0xa3, 0x55, 0xee])
+    host = 0x0a000002  # 10.0.0.2, the frames' destination: the IP checksum stays valid
+    rec, csum, refl, after = run_ref(frames, key, 128, 0, 0, host=(mac, host))
+    assert (refl == (rec[:, 2] == 0x03)).all(), "reflected frames are the ICMP_ECHO records"
+    host2 = 0xc0a80107  # another address: the reference leaves the IP checksum as it was
+    _, _, refl2, after2 = run_ref(frames, key, 128, 0, 0, host=(mac, host2))
+    assert (refl2 == refl).all()
+    tr = traces.pack(frames)
+
+    def laid_out(cat):  # the concatenated frames -> tr's layout (4-aligned starts)
+        out, pos = tr.blob.copy(), 0
+        for o, L in zip(tr.off.astype(np.int64), tr.len.astype(np.int64)):
+            out[o:o + L] = cat[pos:pos + L]
+            pos += L
+        return out
+    after, after2 = laid_out(after), laid_out(after2)
+    np.savez_compressed(os.path.join(HERE, "icmp.npz"), blob=tr.blob, off=tr.off, len=tr.len,
+                        key=np.frombuffer(key, np.uint8), rec=rec, csum=csum, reflected=refl,
+                        mac=np.frombuffer(mac, np.uint8), host_addr=np.uint32(host), after=after,
+                        host_addr2=np.uint32(host2), after2=after2,
+                        note=np.array("frames after eth_input with icmp_reflect's CFG.mac / CFG.host_addr "
+                                      "(host order), two host addresses"))
+    print(f"icmp: {len(frames)} frames, {int(refl.sum())} reflected")
+
+
 def main():
     if not os.path.exists(HARNESS):
         sys.exit("build the harness first: make -C oracle ref")
+    if sys.argv[1:] == ["icmp"]:
+        save_icmp(traces.RSS_KEY)
+        return
     key = traces.RSS_KEY
     rng = np.random.default_rng(0x1B0001)
     edge = edge_frames()
@@ -383,6 +454,7 @@ def main():
     save("fdir", tcp + udp_same + frag_same + badc_hit + edge[:120] + fuzz[:300], key, 64, 2, 0,
          "flow-director filters (FLM -> outbound flow group 8192 + cpu 5), nb_rx_fgs 64, dev_idx 2",
          fdir=filt, cpu=5)
+    save_icmp(key)
 
 
 if __name__ == "__main__":
