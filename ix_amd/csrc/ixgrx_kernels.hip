@@ -1668,7 +1668,7 @@ DEV void slow_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t c
 }
 
 template <bool DMX, bool DRAIN = true>
-DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* buf) {
+DEV void fastc_loop(const KParams& p, uint64_t* __restrict__ T, lds_u32* buf) {
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
@@ -1680,7 +1680,8 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     return c64 < nchunks ? (uint32_t)c64 : nchunks;
   };
   uint32_t c = chunk_of(0);
-  if (c >= nchunks) return;
+  constexpr int kTabV = 12 * 256 / 2 / kBlock;
+  static_assert(kTabV * kBlock == 12 * 256 / 2, "table pieces per thread");
   uint64_t dmask = 0;  // bit k: the wave's k-th chunk was not fixed-shape
   uint32_t kth = 0;
   // readable bytes: up to IXG_TAIL_PAD past the last frame's end
@@ -1694,7 +1695,19 @@ DEV void fastc_loop(const KParams& p, const uint64_t* __restrict__ T, lds_u32* b
     pend.c = kNoDmx;
     sq.n = 0;
   }
+  // the block's hash tables (24 KiB) are staged into LDS with the first
+  // chunk's frame loads already in flight: table loads, frame loads, then
+  // the LDS writes and the barrier (each of the 8 blocks a CU slot runs per
+  // launch paid the staging latency before its first frame load: 0.4 % on
+  // C2, profiles/r04/fstage/). A wave with no chunk still joins the barrier.
+  u32x4 tv[kTabV];
+#pragma unroll
+  for (int k = 0; k < kTabV; k++) tv[k] = reinterpret_cast<const u32x4*>(p.tab)[threadIdx.x + k * kBlock];
   fastc_issue(p, c, nchunks, lim, lane, cur, Lc);
+#pragma unroll
+  for (int k = 0; k < kTabV; k++) reinterpret_cast<u32x4*>(T)[threadIdx.x + k * kBlock] = tv[k];
+  __syncthreads();
+  if (c >= nchunks) return;
   for (;;) {
     const uint32_t cn = chunk_of(kth + 1);
     u32x4 nxt[4];
@@ -1796,7 +1809,6 @@ extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves
 ixg_rx_fastc_s(KParams p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t buf[kWaves][1024];
-  stage_tables(p, T);
   fastc_loop<false>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
 }
 
@@ -1805,7 +1817,6 @@ extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves
 ixg_rx_fastc_dmx_s(KParams p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t buf[kWaves][1024];
-  stage_tables(p, T);
   fastc_loop<true>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
 }
 
