@@ -32,6 +32,30 @@ struct Tables {
   uint32_t n_listen;
 };
 
+// A segment no active or TIME-WAIT pcb took: tcp_in.c:273-304 without
+// SO_REUSE / LWIP_IPV6 (opt.h:1579,2016) breaks at the first lpcb on the
+// port whose address is the segment's destination or ANY; the hlist loop
+// variable keeps the last entry when nothing breaks, so a non-empty list
+// always yields an lpcb (tcp_in.c:317-323); no listener: RST, or nothing for
+// a segment that carries RST itself (tcp_in.c:500-510, TCP_RST = 0x04)
+__device__ __forceinline__ void no_pcb(const Tables& t, uint32_t tflags, uint32_t dst, uint32_t ports, uint32_t& id,
+                                       uint32_t& kind) {
+  const uint32_t dport = ports >> 16;
+  if (t.n_listen != 0) {
+    uint32_t k = 0;
+    for (; k < t.n_listen; k++) {
+      const u32x4 v = reinterpret_cast<const u32x4*>(t.listen)[k];
+      if ((v.y & 0xffffu) == dport && (v.x == dst || v.x == 0u)) break;
+    }
+    if (k == t.n_listen) k = t.n_listen - 1;
+    id = reinterpret_cast<const u32x4*>(t.listen)[k].z;
+    kind = IXG_D_LISTEN;
+  } else {
+    kind = (tflags & 0x04u) ? IXG_D_DROP : IXG_D_RESET;
+    id = 0;
+  }
+}
+
 // tcp_input_find_list (tcp_in.c:122-143): the first entry of [s, e) whose
 // (remote port, local port, remote ip, local ip) equals the segment's
 __device__ __forceinline__ bool find_list(const ixg_pcb_key* __restrict__ ent, uint32_t s, uint32_t e,
@@ -122,26 +146,7 @@ __device__ __forceinline__ void walk_rest(const Tables& t, uint32_t fg, uint32_t
       hit = true;
     }
   }
-  if (!hit) {
-    // tcp_in.c:273-304 without SO_REUSE / LWIP_IPV6 (opt.h:1579,2016): break
-    // at the first lpcb on the port whose address is the segment's
-    // destination or ANY; the hlist loop variable keeps the last entry when
-    // nothing breaks, so a non-empty list always yields an lpcb
-    const uint32_t dport = ports >> 16;
-    if (t.n_listen != 0) {
-      uint32_t k = 0;
-      for (; k < t.n_listen; k++) {
-        const u32x4 v = reinterpret_cast<const u32x4*>(t.listen)[k];
-        if ((v.y & 0xffffu) == dport && (v.x == dst || v.x == 0u)) break;
-      }
-      if (k == t.n_listen) k = t.n_listen - 1;
-      id = reinterpret_cast<const u32x4*>(t.listen)[k].z;
-      kind = IXG_D_LISTEN;  // tcp_in.c:317-323
-    } else {
-      kind = (tflags & 0x04u) ? IXG_D_DROP : IXG_D_RESET;  // tcp_in.c:500-510 (TCP_RST = 0x04)
-      id = 0;
-    }
-  }
+  if (!hit) no_pcb(t, tflags, dst, ports, id, kind);
 }
 
 // A pending lookup's key, one dword: group (14 bits) | PCB bucket << 14 |
@@ -285,26 +290,7 @@ __device__ __forceinline__ void walk(const Tables& t, uint32_t fg, uint32_t buck
       hit = true;
     }
   }
-  if (!hit) {
-    // tcp_in.c:273-304 without SO_REUSE / LWIP_IPV6 (opt.h:1579,2016): break
-    // at the first lpcb on the port whose address is the segment's
-    // destination or ANY; the hlist loop variable keeps the last entry when
-    // nothing breaks, so a non-empty list always yields an lpcb
-    const uint32_t dport = ports >> 16;
-    if (t.n_listen != 0) {
-      uint32_t k = 0;
-      for (; k < t.n_listen; k++) {
-        const u32x4 v = reinterpret_cast<const u32x4*>(t.listen)[k];
-        if ((v.y & 0xffffu) == dport && (v.x == dst || v.x == 0u)) break;
-      }
-      if (k == t.n_listen) k = t.n_listen - 1;
-      id = reinterpret_cast<const u32x4*>(t.listen)[k].z;
-      kind = IXG_D_LISTEN;  // tcp_in.c:317-323
-    } else {
-      kind = (tflags & 0x04u) ? IXG_D_DROP : IXG_D_RESET;  // tcp_in.c:500-510 (TCP_RST = 0x04)
-      id = 0;
-    }
-  }
+  if (!hit) no_pcb(t, tflags, dst, ports, id, kind);
 }
 
 }  // namespace ixgwalk

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--separate", action="store_true",
                     help="time the separate demux pass (ixg_demux_batch_dev) over RX records made once")
     ap.add_argument("--plain", action="store_true", help="time the RX launch alone (no demux) on the same frames")
+    ap.add_argument("--tables", default="established", choices=["established", "mixed", "mixed_nolisten"],
+                    help="bench.py demux_line's table sets")
     args = ap.parse_args()
     import torch
     import bench
@@ -37,11 +39,17 @@ def main():
     tw["id"] += 1 << 20
     tw["remote_port"] ^= 1
     lis = np.array([(0, 80, 0, 7, 0)], dtype=demux.LISTEN_DTYPE)
+    u = np.random.default_rng(2).random(keys.size)
+    act = keys
+    if args.tables != "established":  # 90 % active, 5 % TIME-WAIT, 5 % unknown (bench.py demux_line)
+        act, tw = keys[u < 0.90], keys[(u >= 0.90) & (u < 0.95)]
+        if args.tables == "mixed_nolisten":
+            lis = np.zeros(0, demux.LISTEN_DTYPE)
     s = torch.cuda.current_stream()
     engs, outs = {}, {}
-    for path in args.libs.split(","):
+    for path in args.libs.replace("+", ",").split(","):
         e = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY), lib_path=os.path.join(ROOT, path))
-        demux.load(e, demux.DemuxTables.build(e.cfg, keys, tw, lis))
+        demux.load(e, demux.DemuxTables.build(e.cfg, act, tw, lis))
         engs[os.path.basename(path)] = e
         outs[os.path.basename(path)] = (torch.zeros((wl.n, 16), dtype=torch.uint8, device=dev),
                                         torch.zeros((wl.n, 8), dtype=torch.uint8, device=dev))
@@ -82,7 +90,7 @@ def main():
                "frac80": round(wl.n * 80 / (np.median(t) * 1e-3) / 8e12, 4), "same_as_first": same[v]}
            for v, t in times.items()}
     kind = "plain RX (no demux)" if args.plain else ("separate" if args.separate else "fused") + " demux"
-    print(json.dumps({"workload": kind + " over C2", "results": res}),
+    print(json.dumps({"workload": kind + " over C2, tables " + args.tables, "results": res}),
           flush=True)
 
 
