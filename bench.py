@@ -87,6 +87,16 @@ def alg_bytes(tr, flags: int = 0) -> np.ndarray:
     return rd + desc + 16
 
 
+def lines_touched(lo: np.ndarray, hi: np.ndarray, line: int = 128) -> int:
+    """The distinct `line`-byte lines holding a byte of any range [lo, hi)."""
+    keep = hi > lo
+    lo, hi = lo[keep] // line, (hi[keep] - 1) // line
+    mark = np.zeros(int(hi.max()) + 2, dtype=np.int64)
+    np.add.at(mark, lo, 1)
+    np.add.at(mark, hi + 1, -1)
+    return int((np.cumsum(mark) > 0).sum())
+
+
 def line_floor_bytes(tr, flags: int = 0, line: int = 128) -> float:
     """The bytes per frame a memory system that fetches whole `line`-byte
     lines must move: the distinct lines of the batch that hold a byte the
@@ -101,11 +111,7 @@ def line_floor_bytes(tr, flags: int = 0, line: int = 128) -> float:
     v4 = (b[offs + 16].astype(np.int64) << 8) | b[offs + 17]
     v6 = (b[offs + 18].astype(np.int64) << 8) | b[offs + 19]
     rd = np.minimum(np.where(et == 0x86DD, 54 + v6 if flags & 2 else 14, 14 + v4), tr.len.astype(np.int64))
-    lo, hi = (offs + 12) // line, (offs + np.maximum(rd, 13) - 1) // line
-    mark = np.zeros(int(hi.max()) + 2, dtype=np.int64)
-    np.add.at(mark, lo, 1)
-    np.add.at(mark, hi + 1, -1)
-    lines = int((np.cumsum(mark) > 0).sum())
+    lines = lines_touched(offs + 12, offs + np.maximum(rd, 13), line)
     desc = 2 + (8 if tr.off is not None else 0)
     return lines * line / tr.n + desc + 16
 
@@ -613,10 +619,20 @@ def tcpx_line(dev, steps: int, rank: int, eng_for):
     # bytes the head converts (ports, seqno, ackno, wnd) and the 16-byte ext
     # written; the frame lines they sit in are the frame itself at C2's size
     alg = 16 + 1 + 14 + 16
+    # what a memory system fetching whole 128-B lines must move: the lines
+    # holding the IHL dword (bytes 12..15) and the 20 header bytes from 2
+    # before the TCP header, + the record and the ext (at C2's 60-B stride
+    # every line of the frames holds such a byte)
+    offs = wl.pool.offsets().astype(np.int64)
+    t = offs + 14 + 4 * (wl.pool.blob[offs + 14].astype(np.int64) & 15)
+    nl = lines_touched(np.concatenate([offs + 12, t - 2]), np.concatenate([offs + 16, t + 18]))
+    floor = nl * 128 / wl.pool.n + 32
     check = ("tcpx", wl.pool, wl.out.view(wl.reps, -1, 16)[0].cpu().numpy(), v[0].cpu().numpy(), tiled)
     return {"workload": "tcp_input head rest (seqno/ackno/wnd/tcplen) over C2: 16M x 64B TCP frames; kernel ixg_tcpx_s",
             "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
             "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4),
+            "line_floor_bytes_per_pkt": round(floor, 1),
+            "frac_vs_line_floor": round(floor * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4),
             "gbps_frame_bytes": round((16 + wl.stride + 16) * wl.n / k / 1e9, 1),
             "parity": "tiled-consistent" if tiled else "MISMATCH"}, check
 
@@ -938,6 +954,8 @@ def summary(res: dict) -> dict:
         out["c4"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
     for name, b in res.get("lines", {}).items():
         out[name] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+        if "frac_vs_line_floor" in b:
+            out[name]["frac_line_floor"] = b["frac_vs_line_floor"]
     if "c4_strong" in res:
         b = res["c4_strong"]
         out["c4_strong"] = ent(b["roofline_frac_per_gpu"], b["kernel_ms"], b["mpps_device_resident"], b.get("parity"))
@@ -959,6 +977,8 @@ def summary(res: dict) -> dict:
     if "tcpx" in res:
         b = res["tcpx"]
         out["tcpx"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+        if "frac_vs_line_floor" in b:
+            out["tcpx"]["frac_line_floor"] = b["frac_vs_line_floor"]
     for kind, b in res.get("tx", {}).items():
         out["tx_" + kind] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
     hp = res.get("host_path", {})
