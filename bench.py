@@ -471,6 +471,13 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
     # reads are L2 / Infinity-Cache resident: 64K connections = 1 MiB).
     alg = 16 + 13 + 8 + 16 * 1.0 + 8
     algf = 72 + 8
+    # the separate pass's 128-B line floor: the lines holding byte 14 and the
+    # tuple bytes 26..37 of each frame (at C2's 60-B stride every line of the
+    # frames), the record read, the 8-B result; the bucket lines (64 KiB of
+    # connections: 4 MiB of lines) stay in L2 / Infinity Cache
+    offs = pool.offsets().astype(np.int64)
+    floor = lines_touched(np.concatenate([offs + 14, offs + 26]), np.concatenate([offs + 15, offs + 38])) * 128 \
+        / pool.n + 16 + 8
     res, checks = {"workload": "PCB demux over C2: 16M x 64B TCP frames, 65536 connections; table sets "
                                "established (all ESTABLISHED, 1% other TIME-WAIT entries, 1 listener), mixed "
                                "(90% active, 5% TIME-WAIT, 5% unknown -> listen list), mixed_nolisten (unknown "
@@ -491,7 +498,9 @@ def demux_line(dev, key, steps: int, rank: int, eng_for):
                 "separate": {"kernel": "ixg_demux_s over RX records in HBM (ixg_demux_batch_dev)",
                              "mpps": round(wl.n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
                              "alg_bytes_per_pkt": alg,
-                             "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4)},
+                             "roofline_frac": round(alg * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4),
+                             "line_floor_bytes_per_pkt": round(floor, 1),
+                             "frac_vs_line_floor": round(floor * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4)},
                 "parity": "tiled-consistent" if tiled else "MISMATCH"}
         if name == "established":
             res.update(line)
@@ -965,6 +974,8 @@ def summary(res: dict) -> dict:
                                  d["parity"])
         out["demux_sep"] = ent(d["separate"]["roofline_frac"], d["separate"]["kernel_ms_avg"], d["separate"]["mpps"],
                                d["parity"])
+        if "frac_vs_line_floor" in d["separate"]:
+            out["demux_sep"]["frac_line_floor"] = d["separate"]["frac_vs_line_floor"]
         for name in ("mixed", "mixed_nolisten"):
             if name in d:
                 m = d[name]
