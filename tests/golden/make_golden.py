@@ -98,7 +98,7 @@ def run_ref(frames: list[bytes], key: bytes, nb: int, dev: int, flags: int, fdir
     refl = np.frombuffer(raw, dtype=np.uint8, count=n, offset=o + 4).copy()
     after = np.frombuffer(raw, dtype=np.uint8, count=int(lens.astype(np.int64).sum()), offset=o + 4 + n).copy()
     if host:
-        return rec, csum, refl, after
+        return rec, csum, tcpx, tcpx_hdr, refl, after
     return (rec, csum, tcpx, tcpx_hdr) if full else (rec, csum)
 
 
@@ -378,10 +378,10 @@ def save_icmp(key: bytes):
     frames = frames + [bytes(f) for f in fuzz_frames(rng, 300) if len(f) > 23 and f[23] == 1]
     mac = bytes([0x02, 0x1b, 0x0c, 0xa3, 0x55, 0xee])
     host = 0x0a000002  # 10.0.0.2, the frames' destination: the IP checksum stays valid
-    rec, csum, refl, after = run_ref(frames, key, 128, 0, 0, host=(mac, host))
+    rec, csum, tcpx, tcpx_hdr, refl, after = run_ref(frames, key, 128, 0, 0, host=(mac, host))
     assert (refl == (rec[:, 2] == 0x03)).all(), "reflected frames are the ICMP_ECHO records"
     host2 = 0xc0a80107  # another address: the reference leaves the IP checksum as it was
-    _, _, refl2, after2 = run_ref(frames, key, 128, 0, 0, host=(mac, host2))
+    _, _, _, _, refl2, after2 = run_ref(frames, key, 128, 0, 0, host=(mac, host2))
     assert (refl2 == refl).all()
     tr = traces.pack(frames)
 
@@ -393,7 +393,8 @@ def save_icmp(key: bytes):
         return out
     after, after2 = laid_out(after), laid_out(after2)
     np.savez_compressed(os.path.join(HERE, "icmp.npz"), blob=tr.blob, off=tr.off, len=tr.len,
-                        key=np.frombuffer(key, np.uint8), rec=rec, csum=csum, reflected=refl,
+                        key=np.frombuffer(key, np.uint8), nb_rx_fgs=np.uint16(128), dev_idx=np.uint16(0),
+                        flags=np.uint32(0), rec=rec, csum=csum, tcpx=tcpx, tcpx_hdr=tcpx_hdr, reflected=refl,
                         mac=np.frombuffer(mac, np.uint8), host_addr=np.uint32(host), after=after,
                         host_addr2=np.uint32(host2), after2=after2,
                         note=np.array("frames after eth_input with icmp_reflect's CFG.mac / CFG.host_addr "
