@@ -201,3 +201,67 @@ def test_zero_copy_registered_mbufs(kind):
         eng.unregister_memory(arena.ctypes.data)
     finally:
         eng.close()
+
+
+def _filters_for(tr, pick):
+    """FDIR_DTYPE filters matching frames `pick` of tr (IPv4 TCP)."""
+    offs = tr.offsets().astype(np.int64)
+    b = tr.blob
+    l4 = offs[pick] + 14 + 4 * (b[offs[pick] + 14] & 15).astype(np.int64)
+    f = np.zeros(len(pick), ixgrx.FDIR_DTYPE)
+    f["src_ip"] = b[(offs[pick] + 26)[:, None] + np.arange(4)].view("<u4").reshape(-1)
+    f["dst_ip"] = b[(offs[pick] + 30)[:, None] + np.arange(4)].view("<u4").reshape(-1)
+    f["src_port"] = (b[l4].astype(np.uint16) << 8) | b[l4 + 1]
+    f["dst_port"] = (b[l4 + 2].astype(np.uint16) << 8) | b[l4 + 3]
+    return f
+
+
+def test_set_fdir_with_batches_in_flight():
+    """ixg_rx_set_fdir from IX's connect path while the run loop has batches
+    submitted and not yet polled: frames submitted before the call
+    get the filters in force when they were submitted, frames after it the
+    new ones; every record against the oracle with the matching table."""
+    rng = np.random.default_rng(0x1F0)
+    tr, arena, ptrs = _mbufs("tcp64", 30000, seed=0x1F01)
+    offs = tr.offsets().astype(np.int64)
+    tcp = np.nonzero(tr.blob[offs + 23] == 6)[0]
+    f_old, f_new = _filters_for(tr, tcp[0::5]), _filters_for(tr, tcp[1::5])
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY))
+    try:
+        eng.async_init(batch_frames=4096, max_wait_us=1000000, depth=4, direct=True)
+        eng.set_fdir(f_old, cpu_id=4)
+        half = len(ptrs) // 2
+        got_m, got_r = [], []
+        i = 0
+        while i < half:  # submitted, mostly not polled: batches open and in flight
+            acc = eng.submit_mbufs(ptrs[i:min(i + 64, half)])
+            if acc == 0:
+                m, r = eng.poll(4096, wait=True)
+                got_m.append(m)
+                got_r.append(r)
+            i += acc
+        assert eng.pending() > 0
+        eng.set_fdir(f_new, cpu_id=4)  # the connect path, mid-stream
+        while i < len(ptrs):
+            acc = eng.submit_mbufs(ptrs[i:i + 64])
+            if acc == 0:
+                m, r = eng.poll(4096, wait=True)
+                got_m.append(m)
+                got_r.append(r)
+            i += acc
+        while eng.pending():
+            m, r = eng.poll(4096, wait=True)
+            got_m.append(m)
+            got_r.append(r)
+        m, r = np.concatenate(got_m), np.concatenate(got_r)
+        assert np.array_equal(m, ptrs)
+        rr = r.view(np.uint8).reshape(-1, 16)
+        # (mbuf k holds frame k of tr)
+        e_old = oracle.rx_trace(tr, KEY, threads=8, fdir=f_old, cpu_id=4)[0][:half]
+        e_new = oracle.rx_trace(tr, KEY, threads=8, fdir=f_new, cpu_id=4)[0][half:]
+        assert np.array_equal(rr[:half], e_old), "frames submitted before set_fdir"
+        assert np.array_equal(rr[half:], e_new), "frames submitted after set_fdir"
+        assert ((e_old[:, 3] & 0x20) != 0).sum() > 1000 and ((e_new[:, 3] & 0x20) != 0).sum() > 1000
+    finally:
+        eng.set_fdir(None)
+        eng.close()
