@@ -14,7 +14,7 @@ def main():
     import torch
     import bench
     from ix_amd import ixgrx, traces
-    libs = sys.argv[1].split(",")
+    libs = sys.argv[1].replace("+", ",").split(",")
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     dev = torch.device("cuda:0")
     res = {}
