@@ -8,12 +8,15 @@
 // checksum zero.
 //
 // One wave per 64 records. The record reads are the kernel's traffic when
-// echo requests are rare (IX's case); the wave then takes its echo frames one
-// at a time: all 64 lanes sum the message's dwords (a 1472-byte ping is 6
-// dwords per lane), a cross-lane one's-complement reduction gives the
-// checksum, and 23 lanes write one rewritten header byte each (frames of any
-// alignment). A frame whose message starts at an odd address sums byte-
-// swapped 16-bit words: the folded sum is swapped back (RFC 1071 byte-order
+// echo requests are rare (IX's case). A message of at most kLaneMax bytes
+// (a default 64-byte ping is 64) is rewritten by its own lane: every such
+// lane sums its message's dwords at once, so a flood of small pings costs
+// one pass. Longer messages are taken one at a time by the whole wave: all
+// 64 lanes sum the message's dwords (a 1472-byte ping is 6 dwords per
+// lane), a cross-lane one's-complement reduction gives the checksum, and 23
+// lanes write one rewritten header byte each. Frames may have any
+// alignment: a message that starts at an odd address sums byte-swapped
+// 16-bit words, and the folded sum is swapped back (RFC 1071 byte-order
 // independence).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -27,7 +30,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 
 DEV uint32_t add1c(uint32_t a, uint32_t b) {
@@ -38,6 +40,58 @@ DEV uint32_t add1c(uint32_t a, uint32_t b) {
 DEV uint32_t fold16(uint32_t s) {
   s = (s & 0xffffu) + (s >> 16);
   return (s & 0xffffu) + (s >> 16);
+}
+
+constexpr uint32_t kLaneMax = 128;  // messages a lane rewrites on its own
+
+// dword j of the message's aligned dwords (s: the message's start & 3),
+// with the bytes that do not count zeroed: before the message, the type
+// (message byte 0: becomes 0), the checksum field (bytes 2, 3), past len
+DEV uint32_t msg_word(const uint32_t* w, uint32_t j, uint32_t nd, uint32_t s, uint32_t len) {
+  uint32_t v = w[j];
+  if (j == 0u || j == 1u || j + 1u == nd) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const int t = (int)(4u * j) + k - (int)s;
+      const bool keep = t == 1 || (t >= 4 && t < (int)len);
+      if (!keep) v &= ~(0xffu << (8 * k));
+    }
+  }
+  return v;
+}
+
+// chksum_internet of the folded sum (the swap for an odd start)
+DEV uint32_t icmp_ck(uint32_t acc, uint32_t s) {
+  uint32_t sum = fold16(acc);
+  if (s & 1u) sum = ((sum & 0xffu) << 8) | (sum >> 8);
+  return (~sum) & 0xffffu;
+}
+
+// header byte k (0..22) of the reply: Ethernet dhost = shost, shost =
+// CFG.mac (icmp.c:50-51); IP dst = src, src = CFG.host_addr (:54-55);
+// type = ICMP_ECHOREPLY (:89), checksum (:57-58). Reads before it writes.
+DEV void reply_byte(const ixg_iparams& p, uint8_t* f, uint32_t off, uint32_t ck, int k) {
+  uint32_t at, val;
+  if (k < 6) {
+    at = (uint32_t)k;
+    val = f[6 + k];
+  } else if (k < 12) {
+    at = (uint32_t)k;
+    val = p.mac[k - 6];
+  } else if (k < 16) {
+    at = 30u + (uint32_t)(k - 12);
+    val = f[26 + (k - 12)];
+  } else if (k < 20) {
+    at = 26u + (uint32_t)(k - 16);
+    val = p.host[k - 16];
+  } else if (k == 20) {
+    at = off;
+    val = 0u;
+  } else {
+    at = off + 2u + (uint32_t)(k - 21);
+    val = k == 21 ? (ck & 0xffu) : (ck >> 8);
+  }
+  f[at] = (uint8_t)val;
 }
 
 template <bool OFFS>
@@ -52,7 +106,37 @@ DEV void reflect(const ixg_iparams& p) {
     echo = ((r.x >> 16) & 0xffu) == IXG_V_ICMP_ECHO;
     meta = r.y;
   }
-  for (uint64_t m = __builtin_amdgcn_ballot_w64(echo); m; m &= m - 1u) {
+  // messages of at most kLaneMax bytes: each lane its own
+  if (echo && (meta >> 16) <= kLaneMax) {
+    const uint32_t off = meta & 0xffffu, len = meta >> 16;
+    uint8_t* f = p.base + (OFFS ? p.off[i] : i * (uint64_t)p.stride);
+    const uintptr_t a = reinterpret_cast<uintptr_t>(f) + off;
+    const uint32_t s = (uint32_t)(a & 3u);
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a - s);
+    const uint32_t nd = (s + len + 3u) >> 2;
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < nd; j++) acc = add1c(acc, msg_word(w, j, nd, s, len));
+    const uint32_t ck = icmp_ck(acc, s);
+    // the old source MAC and IP address first: their bytes are rewritten
+    uint8_t src_mac[6], src_ip[4];
+#pragma unroll
+    for (int k = 0; k < 6; k++) src_mac[k] = f[6 + k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) src_ip[k] = f[26 + k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) f[k] = src_mac[k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) f[6 + k] = p.mac[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) f[30 + k] = src_ip[k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) f[26 + k] = p.host[k];
+    f[off] = 0u;
+    f[off + 2u] = (uint8_t)(ck & 0xffu);
+    f[off + 3u] = (uint8_t)(ck >> 8);
+  }
+  const bool big = echo && (meta >> 16) > kLaneMax;
+  for (uint64_t m = __builtin_amdgcn_ballot_w64(big); m; m &= m - 1u) {
     const int e = __builtin_ctzll(m);
     const uint64_t fi = c * 64u + (uint64_t)e;
     const uint32_t fm = __builtin_amdgcn_readlane(meta, e);
@@ -65,51 +149,13 @@ DEV void reflect(const ixg_iparams& p) {
     const uint32_t* w = reinterpret_cast<const uint32_t*>(a - s);
     const uint32_t nd = (s + len + 3u) >> 2;
     uint32_t acc = 0;
-    for (uint32_t j = (uint32_t)lane; j < nd; j += 64u) {
-      uint32_t v = w[j];
-      if (j == 0u || j == 1u || j + 1u == nd) {
-        // keep message bytes 1 (code) and 4 .. len-1: the type (0) and the
-        // checksum field (2, 3) count as zero
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-          const int t = (int)(4u * j) + k - (int)s;
-          const bool keep = t == 1 || (t >= 4 && t < (int)len);
-          if (!keep) v &= ~(0xffu << (8 * k));
-        }
-      }
-      acc = add1c(acc, v);
-    }
+    for (uint32_t j = (uint32_t)lane; j < nd; j += 64u) acc = add1c(acc, msg_word(w, j, nd, s, len));
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) acc = add1c(acc, (uint32_t)__shfl_xor((int)acc, d, 64));
-    uint32_t sum = fold16(acc);
-    if (s & 1u) sum = ((sum & 0xffu) << 8) | (sum >> 8);
-    const uint32_t ck = (~sum) & 0xffffu;  // chksum_internet, stored as is
-    // the header bytes, one lane each: Ethernet dhost = shost, shost =
-    // CFG.mac (icmp.c:50-51); IP dst = src, src = CFG.host_addr (:54-55);
-    // type = ICMP_ECHOREPLY (:89), checksum (:57-58)
-    if (lane < 23) {
-      uint32_t at, val;
-      if (lane < 6) {
-        at = (uint32_t)lane;
-        val = f[6 + lane];
-      } else if (lane < 12) {
-        at = (uint32_t)lane;
-        val = p.mac[lane - 6];
-      } else if (lane < 16) {
-        at = 30u + (uint32_t)(lane - 12);
-        val = f[26 + (lane - 12)];
-      } else if (lane < 20) {
-        at = 26u + (uint32_t)(lane - 16);
-        val = p.host[lane - 16];
-      } else if (lane == 20) {
-        at = off;
-        val = 0u;
-      } else {
-        at = off + 2u + (uint32_t)(lane - 21);
-        val = lane == 21 ? (ck & 0xffu) : (ck >> 8);
-      }
-      f[at] = (uint8_t)val;
-    }
+    const uint32_t ck = icmp_ck(acc, s);  // chksum_internet, stored as is
+    // one header byte per lane (each lane reads its source byte, if any,
+    // before any lane writes: one load instruction, then one store)
+    if (lane < 23) reply_byte(p, f, off, ck, lane);
   }
 }
 

@@ -126,3 +126,26 @@ def test_gpu_reflect_rejects_bad_arguments():
         icmp.reflect_dev(eng, 0, None, 64, 0, 0, bytes(6), 0)  # nothing to do
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+def test_gpu_ping_flood():
+    """A batch of nothing but default-size pings (56-byte payload, 64-byte
+    messages: each lane rewrites its own) and one of 1400-byte pings (the
+    wave takes them one at a time), bit-exact against the oracle."""
+    rng = np.random.default_rng(0x1C4)
+    key = traces.RSS_KEY
+    mac, host = bytes([2, 9, 8, 7, 6, 5]), 0xc0a80001
+    eng = ixgrx.RxEngine(ixgrx.Config(key))
+    try:
+        for pl, n in ((56, 1 << 17), (1400, 1 << 13)):
+            pool = [traces.icmp_echo(rng, pl) for _ in range(512)]
+            tr = traces.pack(pool * (n // 512))
+            er, _ = oracle.rx_trace(tr, key)
+            assert (er[:, 2] == ixgrx.V["ICMP_ECHO"]).all()
+            exp, k = oracle.icmp_reflect_batch(tr.blob, tr.off, 0, er, mac, host)
+            assert k == n
+            out = _dev_reflect(eng, tr.blob, tr.off, 0, er, n, mac, host)
+            assert np.array_equal(out, exp), f"payload {pl}"
+    finally:
+        eng.close()
