@@ -2300,13 +2300,16 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
       hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
       kf = k_fast[lay];
     }
-    // the coalesced kernel runs 8 resident-grids' worth of blocks (each wave
-    // ~8 chunks): 3-4% faster on C2 than one persistent grid (A/B of 1x, 2x,
-    // 3x, 4x, 8x and one chunk per wave, which loses the prefetch: -30%); at
-    // least one block per 64 chunks per wave, so every wave can finish its
-    // own deferred chunks (fastc_loop's DRAIN)
+    // the coalesced kernel runs 16 resident-grids' worth of blocks (each
+    // wave ~4 chunks, two runs of kRunC): with the table staging overlapped
+    // with the first chunk's loads, C2 0.2135 -> 0.2005 ms against 8 grids
+    // (round 4 same-process A/B of 6x .. 64x: 6x 0.2176, 12x 0.2076, 24x
+    // 0.2018, 32x 0.2051, 48x 0.2213, 64x 0.240 ms; the fused demux 0.3057
+    // -> 0.3011 ms; profiles/r04/grid/); at least one block per 64 chunks
+    // per wave, so every wave can finish its own deferred chunks
+    // (fastc_loop's DRAIN)
     const bool fc = kf == ixg_rx_fastc_s || kf == ixg_rx_fastc_dmx_s;
-    const uint32_t gcu = fc ? 8u * ncu : ncu;
+    const uint32_t gcu = fc ? 16u * ncu : ncu;
     if (kf) {
       uint64_t gb = grid_for(kf, wave_blocks, gcu);
       // (a wave takes runs of kRunC chunks: at most 64 / kRunC runs each)
