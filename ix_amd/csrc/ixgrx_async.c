@@ -250,12 +250,8 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 		if (rc)
 			return rc;
 	}
-	for (uint32_t i = 0; i < n; i++) {
-		size_t l;
-		memcpy(&l, mbufs[i], sizeof(l));
-		if (l > IXG_MBUF_DATA_LEN) /* an mbuf holds at most 2048 data bytes (mbuf.h) */
-			return -EINVAL;
-	}
+	if (ixg_check_mbufs(mbufs, n))
+		return -EINVAL;
 	struct ixg_async *a = c->async;
 	if (a->err) {
 		const int e = a->err;
@@ -282,11 +278,11 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 				step = (uint32_t)room;
 			const uint32_t take = a->cfg.batch_frames - b->n - m < step ? a->cfg.batch_frames - b->n - m : step;
 			if (c->nreg && (a->cfg.flags & IXG_ASYNC_DIRECT))
-				b->span = ixg_gather_mbufs_zc(c, b->h_buf, b->span, mbufs + done + m, take,
+				b->span = ixg_gather_mbufs_zc(c, b->h_buf, b->span, mbufs + done + m, take, n - done - m,
 							      b->h_off + b->n + m, b->h_len + b->n + m, &b->nabs);
 			else
-				b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, b->h_off + b->n + m,
-							   b->h_len + b->n + m);
+				b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, n - done - m,
+							   b->h_off + b->n + m, b->h_len + b->n + m);
 			memcpy(b->mbufs + b->n + m, mbufs + done + m, (size_t)take * sizeof(void *));
 			m += take;
 		}

@@ -534,12 +534,26 @@ int ixg_rx_batch_host(void *vctx, const void *frames, const uint64_t *off, const
 
 /* ---- the IX-layout gather ------------------------------ */
 
-size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n, uint64_t *off, uint16_t *len)
+int ixg_check_mbufs(void *const *mbufs, uint32_t n)
+{
+	for (uint32_t i = 0; i < n; i++) {
+		if (i + IXG_MBUF_PREFETCH < n)
+			__builtin_prefetch(mbufs[i + IXG_MBUF_PREFETCH]);
+		size_t l;
+		memcpy(&l, mbufs[i], sizeof(l));
+		if (l > IXG_MBUF_DATA_LEN) /* an mbuf holds at most 2048 data bytes (mbuf.h) */
+			return -EINVAL;
+	}
+	return 0;
+}
+
+size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n, uint32_t avail, uint64_t *off,
+			uint16_t *len)
 {
 	for (uint32_t k = 0; k < n; k++) {
-		if (k + 6 < n) { /* the mbuf header line (len) and the frame's line */
-			__builtin_prefetch(mbufs[k + 6]);
-			__builtin_prefetch((const uint8_t *)mbufs[k + 6] + IXG_MBUF_HEADER_LEN);
+		if (k + IXG_MBUF_PREFETCH < avail) { /* the mbuf header line (len) and the frame's line */
+			__builtin_prefetch(mbufs[k + IXG_MBUF_PREFETCH]);
+			__builtin_prefetch((const uint8_t *)mbufs[k + IXG_MBUF_PREFETCH] + IXG_MBUF_HEADER_LEN);
 		}
 		const uint8_t *mb = (const uint8_t *)mbufs[k];
 		size_t l;
@@ -555,10 +569,12 @@ size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_
 }
 
 size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n,
-			   uint64_t *off, uint16_t *len, uint32_t *nabs)
+			   uint32_t avail, uint64_t *off, uint16_t *len, uint32_t *nabs)
 {
 	uint32_t in_place = 0;
 	for (uint32_t k = 0; k < n; k++) {
+		if (k + IXG_MBUF_PREFETCH < avail) /* the header line: frames read in place need no more */
+			__builtin_prefetch(mbufs[k + IXG_MBUF_PREFETCH]);
 		const uint8_t *mb = (const uint8_t *)mbufs[k];
 		const uintptr_t a = (uintptr_t)mb;
 		size_t l;
@@ -739,12 +755,8 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 		return -EINVAL;
 	if (n == 0)
 		return 0;
-	for (uint32_t i = 0; i < n; i++) {
-		size_t l;
-		memcpy(&l, mbufs[i], sizeof(l));
-		if (l > IXG_MBUF_DATA_LEN) /* an mbuf holds at most 2048 data bytes (mbuf.h) */
-			return -EINVAL;
-	}
+	if (ixg_check_mbufs(mbufs, n))
+		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
 	int rc = 0;
 	uint32_t i = 0, k = 0;
@@ -758,7 +770,8 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 		uint32_t done = 0;
 		while (done < m && span <= IXG_PIPE_BYTES) {
 			const uint32_t step = m - done < 256u ? m - done : 256u;
-			span = ixg_gather_mbufs(sl->h_buf, span, mbufs + i + done, step, sl->h_off + done, sl->h_len + done);
+			span = ixg_gather_mbufs(sl->h_buf, span, mbufs + i + done, step, n - i - done, sl->h_off + done,
+						sl->h_len + done);
 			done += step;
 		}
 		m = done;
