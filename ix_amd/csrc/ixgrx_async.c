@@ -122,6 +122,9 @@ static int batch_alloc(struct ixg_async *a, struct ixg_abatch *b)
 	*b->h_done = 0;
 	HIPCHK(hipMalloc((void **)&b->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 	HIPCHK(hipMemset(b->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)));
+	const int rc = ixg_dstate_reserve(&b->ds, ((size_t)nf + 63u) / 64u);
+	if (rc)
+		return rc;
 	HIPCHK(hipHostMalloc((void **)&b->h_buf, bcap, hipHostMallocDefault));
 	HIPCHK(hipHostMalloc((void **)&b->h_rec, (size_t)nf * sizeof(struct ixg_rx_rec), hipHostMallocDefault));
 	if (!(a->cfg.flags & IXG_ASYNC_DIRECT)) {

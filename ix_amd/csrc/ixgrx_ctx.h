@@ -131,6 +131,9 @@ IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const u
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t lflags, hipStream_t s);
 IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
+/* the per-chunk defer flags for batches of up to nchunks chunks (grown, never
+ * shrunk; growing frees the old buffer, which waits for the device) */
+IXG_INTERNAL int ixg_dstate_reserve(struct ixg_dstate *ds, size_t nchunks);
 
 /* The IX-layout gather both host paths use: frames out of mbufs (len =
  * size_t at +0, data at +64, inc/ix/mbuf.h:73-90) into staging, the MAC

@@ -239,6 +239,22 @@ fail:
 
 /* ---- batches --------------------------------------------------------------- */
 
+int ixg_dstate_reserve(struct ixg_dstate *ds, size_t nchunks)
+{
+	if (nchunks <= ds->defer_cap)
+		return 0;
+	/* hipFree waits for the whole device, i.e. for every other thread's
+	 * launches too: the host paths reserve their largest batch when they
+	 * allocate (ixgrx_async.c batch_alloc, slot_init) */
+	hipFree(ds->d_defer);
+	ds->d_defer = NULL;
+	ds->defer_cap = 0;
+	const size_t cap = nchunks + nchunks / 4 + 64;
+	HIPCHK(hipMalloc((void **)&ds->d_defer, cap));
+	ds->defer_cap = cap;
+	return 0;
+}
+
 int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t overlap, hipStream_t s)
@@ -277,15 +293,10 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 	}
 	size_t nchunks = ((size_t)n + 63) / 64;
 	if (!c->force_general) {
-		if (nchunks > ds->defer_cap) {
-			/* grows once per larger batch; not inside a graph capture */
-			hipFree(ds->d_defer);
-			ds->d_defer = NULL;
-			ds->defer_cap = 0;
-			size_t cap = nchunks + nchunks / 4 + 64;
-			HIPCHK(hipMalloc((void **)&ds->d_defer, cap));
-			ds->defer_cap = cap;
-		}
+		/* grows once per larger batch; not inside a graph capture */
+		int rc = ixg_dstate_reserve(ds, nchunks);
+		if (rc)
+			return rc;
 		p.defer = ds->d_defer;
 		p.present = ds->d_present;
 		if (++ds->epoch == 0)
@@ -676,6 +687,9 @@ static int slot_init(struct ixg_slot *sl)
 		HIPCHK(hipMalloc((void **)&sl->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 		HIPCHK(hipMemset(sl->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 	}
+	int rc = ixg_dstate_reserve(&sl->ds, (IXG_PIPE_FRAMES + 63u) / 64u);
+	if (rc)
+		return rc;
 	const size_t bcap = IXG_STAGE_BYTES(IXG_PIPE_BYTES + 256u * 2048u, IXG_PIPE_FRAMES), ncap = IXG_PIPE_FRAMES;
 	if (!sl->h_buf)
 		HIPCHK(hipHostMalloc((void **)&sl->h_buf, bcap, hipHostMallocDefault));
