@@ -214,8 +214,11 @@ hipError_t hipHostMalloc(void **p, size_t n, unsigned int f)
 	(void)f;
 	return hipMalloc(p, n);
 }
+static unsigned long g_frees; /* hipFree of an allocation (a device-wide wait on HIP) */
+unsigned long fakehip_frees(void) { return g_frees; }
 hipError_t hipFree(void *p)
 {
+	g_frees += p != NULL;
 	mem_del(p);
 	free(p);
 	return hipSuccess;

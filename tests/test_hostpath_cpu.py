@@ -156,6 +156,31 @@ def test_async_aggregates_iterations(fake):
     assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
 
 
+@pytest.mark.parametrize("direct", [True, False])
+def test_launches_never_free(fake, direct):
+    """hipFree waits for the whole device, i.e. for every other thread's
+    batches: batches growing from 1 frame to batch_frames, and synchronous
+    calls up to a pipeline chunk, must not free (grow) a device buffer."""
+    fake.lib.fakehip_frees.restype = ctypes.c_ulong
+    tr, arena, ptrs = _mbufs("tcp64", 140000, seed=12)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=4096, batch_bytes=1 << 22, max_wait_us=10000000, depth=2, direct=direct)
+        f0 = fake.lib.fakehip_frees()
+        i = 0
+        for k in (1, 65, 700, 4096):
+            assert eng.submit_mbufs(ptrs[i:i + k]) == k
+            eng.flush()
+            m, r = eng.poll(k, wait=True)
+            assert np.array_equal(m, ptrs[i:i + k])
+            i += k
+        for k in (1, 2000, 131072):
+            eng.batch_mbufs(ptrs[:k])
+        assert fake.lib.fakehip_frees() == f0
+    finally:
+        eng.close()
+
+
 def test_async_back_pressure_flush_and_busy(fake):
     tr, arena, ptrs = _mbufs("imix", 400, seed=11)
     eng = fake()
