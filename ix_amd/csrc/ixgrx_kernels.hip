@@ -2206,8 +2206,11 @@ DEV void short_span_body(const KParams& p) {
 #define IXG_SPAN_KERNEL(NAME, OFFS, DMX, ...)                                                                  \
   extern "C" __global__ void __launch_bounds__(64 * kSpanWaves) __attribute__((amdgpu_waves_per_eu(4))) \
   NAME(KParams p) { short_span_body<OFFS, DMX, ##__VA_ARGS__>(p); }
-IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false)
-IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false)
+// span copies non-temporal (AUX 2: each span is read once, out of LDS):
+// C5 0.4343 -> 0.4275 ms, c5r 0.4138 -> 0.3960, C3 unchanged in a
+// same-process A/B (profiles/r04/span_nt/)
+IXG_SPAN_KERNEL(ixg_rx_short_sp_s, false, false, 2)
+IXG_SPAN_KERNEL(ixg_rx_short_sp_o, true, false, 2)
 
 
 // The sampler: one block picks the launch's IXG_MODE_*: FAST when at least
