@@ -45,11 +45,14 @@ DEV Ev classify(const EParams& p, uint32_t i) {
   Ev e;
   const bool valid = i < p.n;
   const uint32_t ic = valid ? i : 0u;
-  e.rec = reinterpret_cast<const u32x4*>(p.rec)[ic];
+  // non-temporal: the records and demux results are streamed through once
+  // per pass (events 0.2934 -> 0.2825 ms in a same-process A/B,
+  // profiles/r04/ev_nt/)
+  e.rec = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p.rec) + ic);
   const uint32_t verdict = (e.rec.x >> 16) & 0xffu;
   const uint32_t plen = e.rec.y >> 16;
   u32x2 d = {0u, 0u};
-  if (p.dmx) d = reinterpret_cast<const u32x2*>(p.dmx)[ic];
+  if (p.dmx) d = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p.dmx) + ic);
   e.id = d.x;
   const uint32_t dkind = d.y & 0xffu;
   const bool udp = verdict == IXG_V_UDP;
