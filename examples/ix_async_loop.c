@@ -24,12 +24,23 @@
  *   cfg_frames= cfg_bytes= cfg_wait_us= cfg_depth= direct=0|1 dump=FILE
  *   register=1: register each thread's mbuf arena (ixg_rx_register_memory)
  *   so the kernels read the frames in place (zero copy)
+ *   idle=wait|spin: an iteration whose frames the full ring refused either
+ *   waits in ixg_rx_poll for the oldest batch (wait, the default: the CPU
+ *   has no RX work until a batch returns, and gives its time away) or polls
+ *   again at once (spin). On a CPU quota (the GPU box: 16 CPUs per 100 ms),
+ *   16 spinning threads plus the HIP runtime's own got the process throttled
+ *   for ~10 ms at a time.
  * FRAMES_FILE: u32 count, u16 lengths[count], then the frames back to back.
  * dump=FILE (loop mode): thread 0's first `count` records, in submission
  * order, for the caller's parity check against the oracle.
  */
 #define _GNU_SOURCE
+#include <execinfo.h>
+#include <fcntl.h>
 #include <pthread.h>
+#include <ucontext.h>
+#include <signal.h>
+#include <unistd.h>
 #include <sys/resource.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -48,14 +59,60 @@ static double now_s(void)
 	return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
 }
 
+/* A fault anywhere in the process (the library, the HIP runtime, a
+ * profiler's interception) prints the fault address, the stack and the
+ * process's mappings, so every frame can be resolved to a library and an
+ * offset afterwards (a SIGSEGV under rocprofv3 whose runtime
+ * frames could not be attributed). Only async-signal-safe calls. */
+static void fault_dump(int sig, siginfo_t *si, void *uc)
+{
+	char b[160];
+	const void *pc = NULL;
+#if defined(__x86_64__)
+	if (uc)
+		pc = (const void *)((ucontext_t *)uc)->uc_mcontext.gregs[REG_RIP];
+#endif
+	int n = snprintf(b, sizeof(b), "\n*** ix_async_loop: signal %d at address %p, pc %p, thread %d; stack:\n", sig,
+			 si ? si->si_addr : NULL, pc, (int)gettid());
+	if (write(2, b, (size_t)n) < 0)
+		_exit(128 + sig);
+	void *fr[64];
+	backtrace_symbols_fd(fr, backtrace(fr, 64), 2);
+	if (write(2, "/proc/self/maps:\n", 17) < 0)
+		_exit(128 + sig);
+	const int fd = open("/proc/self/maps", O_RDONLY);
+	if (fd >= 0) {
+		char m[4096];
+		ssize_t k;
+		while ((k = read(fd, m, sizeof(m))) > 0)
+			if (write(2, m, (size_t)k) < 0)
+				break;
+		close(fd);
+	}
+	signal(sig, SIG_DFL);
+	raise(sig);
+}
+
+static void install_fault_dump(void)
+{
+	void *fr[4];
+	backtrace(fr, 4); /* loads the unwinder now, not inside the handler */
+	struct sigaction sa;
+	memset(&sa, 0, sizeof(sa));
+	sa.sa_sigaction = fault_dump;
+	sa.sa_flags = SA_SIGINFO | SA_RESETHAND;
+	sigaction(SIGSEGV, &sa, NULL);
+	sigaction(SIGBUS, &sa, NULL);
+}
+
 /* ---- options ------------------------------------------------------------- */
 static struct {
 	const char *frames, *mode, *dump;
-	int threads, batch, device, direct, reg;
+	int threads, batch, device, direct, reg, spin;
 	double seconds;
 	uint32_t n, arena;
 	struct ixg_rx_async_cfg acfg;
-} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 2.0, 64, 1u << 16,
+} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 0, 2.0, 64, 1u << 16,
 	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}};
 
 static const uint8_t rss_key[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
@@ -200,6 +257,7 @@ static void *work(void *arg)
 	struct rusage ru0;
 	getrusage(RUSAGE_THREAD, &ru0);
 	double t_prev = now_s();
+	int last_acc = 1;
 	for (;;) {
 		const double t = now_s();
 		if (t - t_prev > w->max_gap)
@@ -216,6 +274,7 @@ static void *work(void *arg)
 				w->rc = acc;
 				break;
 			}
+			last_acc = acc;
 			if (acc > 0) {
 				sub += (uint64_t)acc;
 				pos = (pos + (uint32_t)acc) % n;
@@ -229,7 +288,10 @@ static void *work(void *arg)
 		} else if (got == sub) {
 			break;
 		}
-		int r = ixg_rx_poll(w->ctx, pm, pr, POLL_MAX, more ? 0 : 1);
+		/* frames refused by a full ring: nothing to do for RX until the
+		 * oldest batch returns */
+		const int idle = more && last_acc == 0 && !opt.spin;
+		int r = ixg_rx_poll(w->ctx, pm, pr, POLL_MAX, more && !idle ? 0 : 1);
 		if (r < 0) {
 			w->rc = r;
 			break;
@@ -362,7 +424,16 @@ static int run_loop(void)
 	uint64_t staged = 0;
 	int uniform = 1;
 	for (uint32_t i = 0; i < pool_n; i++) {
-		staged += pool_len[i] > 12 ? ((pool_len[i] - 12u + 3u) & ~3u) : 0u;
+		/* the library stages bytes [12, E): E = max(14 + ip_len, l4 + 20)
+		 * for IPv4 frames, capped at L (ixgrx_ctx.h ixg_stage_ext) */
+		const uint8_t *f = pool_frame[i];
+		uint32_t e = pool_len[i];
+		if (e >= 34 && f[12] == 0x08 && f[13] == 0 && (f[14] >> 4) == 4) {
+			uint32_t x = 14u + ((uint32_t)f[16] << 8 | f[17]), h = 14u + 4u * (f[14] & 15u) + 20u;
+			x = x > h ? x : h;
+			e = x < e ? x : e;
+		}
+		staged += e > 12 ? ((e - 12u + 3u) & ~3u) : 0u;
 		uniform &= pool_len[i] == pool_len[0];
 	}
 	const double staged_b = opt.reg ? 10.0 : (double)staged / pool_n + 2.0 + (uniform ? 0.0 : 8.0);
@@ -484,6 +555,7 @@ int main(int argc, char **argv)
 		fprintf(stderr, "usage: %s FRAMES_FILE loop|sync|async1 [key=value ...]\n", argv[0]);
 		return 2;
 	}
+	install_fault_dump();
 	opt.frames = argv[1];
 	opt.mode = argv[2];
 	for (int i = 3; i < argc; i++) {
@@ -505,6 +577,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(k, "cfg_depth")) opt.acfg.depth = (uint32_t)atoi(v);
 		else if (!strcmp(k, "direct")) opt.acfg.flags = atoi(v) ? IXG_ASYNC_DIRECT : 0;
 		else if (!strcmp(k, "register")) opt.reg = atoi(v);
+		else if (!strcmp(k, "idle")) opt.spin = !strcmp(v, "spin");
 		else {
 			fprintf(stderr, "unknown option %s\n", k);
 			return 2;

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/prctl.h>
 
 #include "ixgrx_ctx.h"
 
@@ -45,6 +46,8 @@ struct ixg_abatch {
 	uint32_t nabs;       /* frames read in place (registered memory) */
 	uint32_t n, taken;   /* frames held, frames already returned by poll */
 	size_t span;         /* gathered bytes (ixg_gather_mbufs) */
+	size_t hi;           /* the furthest gathered frame's end (ixg_stage_finish) */
+	size_t link;         /* bytes of the in-place frames (host-link reads) */
 	uint8_t *h_buf, *d_buf;
 	uint64_t *h_off;
 	uint16_t *h_len;
@@ -192,9 +195,9 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	HIPCHK(hipSetDevice(c->device));
 	struct ixg_stage st;
 	if (b->nabs)
-		ixg_stage_finish_abs(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
+		ixg_stage_finish_abs(b->h_buf, b->span, b->hi, b->h_off, b->h_len, b->n, &st);
 	else
-		ixg_stage_finish(b->h_buf, b->span, b->h_off, b->h_len, b->n, &st);
+		ixg_stage_finish(b->h_buf, b->span, b->hi, b->h_off, b->h_len, b->n, &st);
 	const int direct = (a->cfg.flags & IXG_ASYNC_DIRECT) != 0;
 	const uint64_t t0 = tsc();
 	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, b->stream);
@@ -210,7 +213,7 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 		return rc;
 	b->state = AS_INFLIGHT;
 	a->st.batches++;
-	if (b->n < a->cfg.batch_frames && b->span < a->cfg.batch_bytes)
+	if (b->n < a->cfg.batch_frames && b->span + b->link < a->cfg.batch_bytes)
 		a->st.batches_by_time++;
 	return 0;
 }
@@ -231,15 +234,19 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
 	b->t_open = t;
 	b->n = b->taken = 0;
 	b->nabs = 0;
-	b->span = 0;
+	b->span = b->hi = b->link = 0;
 	a->tail = (a->tail + 1) % a->cfg.depth;
 	a->count++;
 	return b;
 }
 
+/* batch_bytes counts the bytes the kernels read over the host link: the
+ * staged ones and the in-place frames' (a zero-copy batch of 1514-B frames
+ * that counted only its ~10 staged bytes per frame closed at 16384 frames,
+ * 25 MB of link reads, and queued its frames for 12 ms at 16 threads) */
 static int due(const struct ixg_async *a, const struct ixg_abatch *b, uint64_t t)
 {
-	return b->n >= a->cfg.batch_frames || b->span >= a->cfg.batch_bytes ||
+	return b->n >= a->cfg.batch_frames || b->span + b->link >= a->cfg.batch_bytes ||
 	       t - b->t_open >= (uint64_t)a->cfg.max_wait_us * 1000u;
 }
 
@@ -272,20 +279,21 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 		 * may pass the byte limit: bytes_cap leaves room for it) */
 		uint32_t m = 0;
 		const uint64_t g0 = tsc();
-		while (done + m < n && b->n + m < a->cfg.batch_frames && b->span < a->cfg.batch_bytes) {
+		while (done + m < n && b->n + m < a->cfg.batch_frames && b->span + b->link < a->cfg.batch_bytes) {
 			/* at most as many frames as can still start below batch_bytes
-			 * (each stages at most IXG_MBUF_DATA_LEN - 12 bytes) */
-			const size_t room = (a->cfg.batch_bytes - b->span) / (IXG_MBUF_DATA_LEN - 12u) + 1u;
+			 * (each stages or reads at most IXG_MBUF_DATA_LEN - 12 bytes) */
+			const size_t room = (a->cfg.batch_bytes - b->span - b->link) / (IXG_MBUF_DATA_LEN - 12u) + 1u;
 			uint32_t step = n - done - m < 16u ? n - done - m : 16u;
 			if (step > room)
 				step = (uint32_t)room;
 			const uint32_t take = a->cfg.batch_frames - b->n - m < step ? a->cfg.batch_frames - b->n - m : step;
 			if (c->nreg && (a->cfg.flags & IXG_ASYNC_DIRECT))
 				b->span = ixg_gather_mbufs_zc(c, b->h_buf, b->span, mbufs + done + m, take, n - done - m,
-							      b->h_off + b->n + m, b->h_len + b->n + m, &b->nabs);
+							      b->h_off + b->n + m, b->h_len + b->n + m, &b->hi, &b->nabs,
+							      &b->link);
 			else
 				b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, n - done - m,
-							   b->h_off + b->n + m, b->h_len + b->n + m);
+							   b->h_off + b->n + m, b->h_len + b->n + m, &b->hi);
 			memcpy(b->mbufs + b->n + m, mbufs + done + m, (size_t)take * sizeof(void *));
 			m += take;
 		}
@@ -330,15 +338,82 @@ int ixg_async_quiesce(struct ixg_ctx *c)
 	struct ixg_async *a = c->async;
 	if (!a || !a->count)
 		return 0;
-	/* the OPEN batch goes now, with the state its frames were submitted under */
+	/* the OPEN batch goes now, with the state its frames were submitted under;
+	 * once it is launched, an earlier failed launch of it is not reported
+	 * again (its frames are in flight) */
 	int rc = launch_open(c, a);
 	if (rc)
 		return rc;
+	a->err = 0;
 	for (uint32_t k = 0, i = a->head; k < a->count; k++, i = (i + 1) % a->cfg.depth)
 		if (a->b[i].state == AS_INFLIGHT) {
 			HIPCHK(hipSetDevice(c->device));
 			HIPCHK(hipStreamSynchronize(a->b[i].stream));
 		}
+	return 0;
+}
+
+/* Block until batch b's completion word holds its sequence number: a short
+ * spin, then naps that give the CPU away. On the GPU box (a cgroup quota of
+ * 16 CPUs) 16 threads that spin while their rings are full, plus the HIP
+ * runtime's own threads, got the whole process throttled for ~10 ms at a
+ * time (cpu.stat nr_throttled 29 in 3 s). One stream query
+ * per wait (not per poll) reports a failed stream early; past
+ * IXG_WAIT_RUNTIME_NS the runtime's own wait decides, so a batch whose
+ * kernels failed returns -EIO instead of waiting forever. */
+#ifndef IXG_WAIT_NAP_NS
+#define IXG_WAIT_NAP_NS 10000L
+#endif
+/* the naps' timer slack while waiting (the default 50 us would make a 10 us
+ * nap ~60 us; the caller's slack is restored after the wait) */
+#ifndef IXG_WAIT_SLACK_NS
+#define IXG_WAIT_SLACK_NS 2000L
+#endif
+#ifndef IXG_WAIT_SPIN
+#define IXG_WAIT_SPIN 256u
+#endif
+#define IXG_WAIT_RUNTIME_NS 200000000ull
+static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, int *napped)
+{
+	for (uint32_t k = 0;; k++) {
+		if (__atomic_load_n(b->h_done, __ATOMIC_ACQUIRE) == b->seq)
+			return 0;
+		if (k < IXG_WAIT_SPIN) {
+#if defined(__x86_64__)
+			__builtin_ia32_pause();
+#endif
+			continue;
+		}
+		if (k == IXG_WAIT_SPIN) {
+			HIPCHK(hipSetDevice(c->device));
+			const hipError_t e = hipStreamQuery(b->stream);
+			if (e != hipSuccess && e != hipErrorNotReady)
+				return -EIO;
+			continue;
+		}
+		if (now_ns() - t0 > IXG_WAIT_RUNTIME_NS)
+			return 1;
+		if (!*napped && IXG_WAIT_SLACK_NS > 0) {
+			*napped = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+			prctl(PR_SET_TIMERSLACK, (unsigned long)IXG_WAIT_SLACK_NS, 0, 0, 0);
+		}
+		*napped |= 1 << 30;
+		const struct timespec nap = {0, IXG_WAIT_NAP_NS};
+		nanosleep(&nap, NULL);
+	}
+}
+
+static int wait_done(struct ixg_ctx *c, struct ixg_abatch *b)
+{
+	int napped = 0; /* the caller's timer slack (+ 1 << 30) once naps began */
+	const int rc = wait_word(c, b, now_ns(), &napped);
+	if (napped && IXG_WAIT_SLACK_NS > 0)
+		prctl(PR_SET_TIMERSLACK, (unsigned long)(napped & ~(1 << 30)), 0, 0, 0);
+	if (rc <= 0)
+		return rc;
+	HIPCHK(hipSetDevice(c->device));
+	if (hipStreamSynchronize(b->stream) != hipSuccess || __atomic_load_n(b->h_done, __ATOMIC_ACQUIRE) != b->seq)
+		return -EIO;
 	return 0;
 }
 
@@ -376,11 +451,10 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 				if (!wait || got)
 					break;
 				const uint64_t w0 = tsc();
-				HIPCHK(hipSetDevice(c->device));
-				const hipError_t e = hipStreamSynchronize(b->stream);
+				const int rc = wait_done(c, b);
 				a->st.wait_ns += tsc() - w0;
-				if (e != hipSuccess || __atomic_load_n(b->h_done, __ATOMIC_ACQUIRE) != b->seq)
-					return -EIO;
+				if (rc)
+					return rc;
 			}
 			b->state = AS_DONE;
 		}

@@ -135,15 +135,39 @@ IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
  * shrunk; growing frees the old buffer, which waits for the device) */
 IXG_INTERNAL int ixg_dstate_reserve(struct ixg_dstate *ds, size_t nchunks);
 
+/* The bytes of a frame the path can read: [0, ixg_stage_ext(f, L)). For an
+ * IPv4 frame (ethertype 0x0800, version 4) nothing past
+ * max(14 + ip_len, l4 + 20), l4 = 14 + 4 ihl, is read by any check or sum:
+ * ip_input's checks read the header (dp/net/ip.c:63-87), the L4 sums and
+ * tcp_input / udp_input / icmp_input stop at the IP total length
+ * (dp/lwip/misc.c:57-67, dp/net/udp.c:53-60, dp/net/icmp.c:78-92), and the
+ * NIC's RSS reads the ports at l4 (a TCP header's 20 bytes cover the doff and
+ * flags a record reports even for a short segment). The Ethernet pad past
+ * 14 + ip_len (C2's 64-B frames: 6 bytes) is therefore not staged. Other
+ * frames (ARP, IPv6, anything dropped on the ethertype): all L bytes. */
+static inline size_t ixg_stage_ext(const uint8_t *f, size_t L)
+{
+	if (L < 34 || f[12] != 0x08 || f[13] != 0x00 || (f[14] >> 4) != 4)
+		return L;
+	size_t e = 14u + (((size_t)f[16] << 8) | f[17]);
+	const size_t h = 14u + 4u * (size_t)(f[14] & 15u) + 20u;
+	if (e < h)
+		e = h;
+	return e < L ? e : L;
+}
+
 /* The IX-layout gather both host paths use: frames out of mbufs (len =
  * size_t at +0, data at +64, inc/ix/mbuf.h:73-90) into staging, the MAC
  * addresses (bytes 0..11, which nothing on the path reads) skipped. Frame k
- * of the run gets the 4-aligned offset pos[k] and its bytes [12, L) land at
- * frames + pos[k] + 12; pos[k+1] = pos[k] + round4(max(L, 12) - 12), so a
- * frame's bytes 0..11 overlap its predecessor's tail. Writes n offsets and
- * lengths, returns the staged span (pos of the frame after the last). */
+ * of the run gets the 4-aligned offset pos[k] and its bytes [12, E) land at
+ * frames + pos[k] + 12, E = ixg_stage_ext(frame, L); pos[k+1] = pos[k] +
+ * round4(max(E, 12) - 12), so a frame's bytes 0..11 overlap its
+ * predecessor's tail, and its bytes [E, L), which nothing reads, are the
+ * next frame's. Writes n offsets and lengths, returns the staged span (pos
+ * of the frame after the last) and raises *hi to the end of the furthest
+ * frame (pos[k] + L): the image's readable bytes must reach it. */
 IXG_INTERNAL size_t ixg_gather_mbufs(uint8_t *frames, size_t pos0, void *const *mbufs, uint32_t n, uint32_t avail,
-				     uint64_t *off, uint16_t *len);
+				     uint64_t *off, uint16_t *len, size_t *hi);
 
 /* How many mbufs ahead the gathers prefetch (the header line with mbuf->len
  * and the frame's first line): `avail` (>= n) is how many valid pointers
@@ -159,18 +183,24 @@ IXG_INTERNAL int ixg_check_mbufs(void *const *mbufs, uint32_t n);
  * frame whose mbuf lies in one of c's registered regions is not copied; its
  * off[k] is its data's device address | IXG_OFF_ABS. Other frames are
  * gathered as by ixg_gather_mbufs (off[k] = staging position). Returns the
- * staged span; *nabs counts the in-place frames. */
+ * staged span; *nabs counts the in-place frames and *link grows by the bytes
+ * the kernels will read of them over the host link (their lengths, rounded
+ * up to 64-byte requests). */
 #define IXG_OFF_ABS (1ull << 63)
 IXG_INTERNAL size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos, void *const *mbufs,
-				       uint32_t n, uint32_t avail, uint64_t *off, uint16_t *len, uint32_t *nabs);
+				       uint32_t n, uint32_t avail, uint64_t *off, uint16_t *len, size_t *hi,
+				       uint32_t *nabs, size_t *link);
 
-IXG_INTERNAL void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint16_t *len, uint32_t n,
-		      struct ixg_stage *st);
+/* lay out the image of a gathered run (span, hi: ixg_gather_mbufs): a fixed
+ * stride when the offsets are k * stride, else the u64 offsets */
+IXG_INTERNAL void ixg_stage_finish(uint8_t *buf, size_t span, size_t hi, const uint64_t *off, const uint16_t *len,
+				  uint32_t n, struct ixg_stage *st);
 /* the same for a run with in-place frames (ixg_gather_mbufs_zc, nabs > 0):
- * every offset becomes relative to st->base, the lowest frame address of the
- * run (staged frames: buf's device address + position) */
-IXG_INTERNAL void ixg_stage_finish_abs(uint8_t *buf, size_t span, uint64_t *off, const uint16_t *len, uint32_t n,
-				      struct ixg_stage *st);
+ * the image's offsets are relative to st->base, the lowest frame address of
+ * the run (staged frames: buf's device address + position). off[] is left as
+ * gathered, so a launch that fails can lay the run out again. */
+IXG_INTERNAL void ixg_stage_finish_abs(uint8_t *buf, size_t span, size_t hi, const uint64_t *off,
+				      const uint16_t *len, uint32_t n, struct ixg_stage *st);
 
 /* enqueue one staged image on `s`: its H2D copy, the kernels, the D2H copy
  * of the records into h_rec; direct: the kernels read the pinned image and

@@ -558,8 +558,21 @@ int ixg_check_mbufs(void *const *mbufs, uint32_t n)
 	return 0;
 }
 
+/* one frame into the staging at pos: its bytes [12, ixg_stage_ext) */
+static inline size_t gather_one(uint8_t *frames, size_t pos, const uint8_t *mb, size_t l, size_t *hi)
+{
+	if (pos + l > *hi)
+		*hi = pos + l;
+	if (l <= 12)
+		return pos;
+	const uint8_t *f = mb + IXG_MBUF_HEADER_LEN;
+	const size_t e = ixg_stage_ext(f, l);
+	memcpy(frames + pos + 12, f + 12, e - 12);
+	return pos + ((e - 12 + 3) & ~(size_t)3);
+}
+
 size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n, uint32_t avail, uint64_t *off,
-			uint16_t *len)
+			uint16_t *len, size_t *hi)
 {
 	for (uint32_t k = 0; k < n; k++) {
 		if (k + IXG_MBUF_PREFETCH < avail) { /* the mbuf header line (len) and the frame's line */
@@ -571,18 +584,16 @@ size_t ixg_gather_mbufs(uint8_t *frames, size_t pos, void *const *mbufs, uint32_
 		memcpy(&l, mb, sizeof(l)); /* mbuf->len (inc/ix/mbuf.h:75) */
 		off[k] = pos;
 		len[k] = (uint16_t)l;
-		if (l > 12) {
-			memcpy(frames + pos + 12, mb + IXG_MBUF_HEADER_LEN + 12, l - 12);
-			pos += (l - 12 + 3) & ~(size_t)3;
-		}
+		pos = gather_one(frames, pos, mb, l, hi);
 	}
 	return pos;
 }
 
 size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos, void *const *mbufs, uint32_t n,
-			   uint32_t avail, uint64_t *off, uint16_t *len, uint32_t *nabs)
+			   uint32_t avail, uint64_t *off, uint16_t *len, size_t *hi, uint32_t *nabs, size_t *link)
 {
 	uint32_t in_place = 0;
+	size_t lb = 0;
 	for (uint32_t k = 0; k < n; k++) {
 		if (k + IXG_MBUF_PREFETCH < avail) /* the header line: frames read in place need no more */
 			__builtin_prefetch(mbufs[k + IXG_MBUF_PREFETCH]);
@@ -601,56 +612,67 @@ size_t ixg_gather_mbufs_zc(const struct ixg_ctx *c, uint8_t *frames, size_t pos,
 		if (r < c->nreg && !(a & 3)) {
 			off[k] = ((uint64_t)(a + IXG_MBUF_HEADER_LEN) + (uint64_t)c->reg[r].delta) | IXG_OFF_ABS;
 			in_place++;
+			lb += (l + 63u) & ~(size_t)63;
 			continue;
 		}
 		off[k] = pos;
-		if (l > 12) {
-			memcpy(frames + pos + 12, mb + IXG_MBUF_HEADER_LEN + 12, l - 12);
-			pos += (l - 12 + 3) & ~(size_t)3;
-		}
+		pos = gather_one(frames, pos, mb, l, hi);
 	}
 	*nabs += in_place;
+	*link += lb;
 	return pos;
 }
 
-void ixg_stage_finish_abs(uint8_t *buf, size_t span, uint64_t *off, const uint16_t *len, uint32_t n,
+/* the end of the image's frame bytes: the staged span, the furthest frame
+ * end (a frame's bytes past ixg_stage_ext are not staged, but the kernels'
+ * loads may reach them), then IXG_TAIL_PAD zero bytes; returns where the
+ * offsets / lengths may start */
+static size_t frames_tail(uint8_t *buf, size_t span, size_t hi)
+{
+	const size_t end = span + 12 > hi ? span + 12 : hi;
+	memset(buf + span + 12, 0, end - (span + 12) + IXG_TAIL_PAD + 16);
+	return (end + IXG_TAIL_PAD + 16 + 7) & ~(size_t)7;
+}
+
+void ixg_stage_finish_abs(uint8_t *buf, size_t span, size_t hi, const uint64_t *off, const uint16_t *len, uint32_t n,
 			  struct ixg_stage *st)
 {
-	memset(buf + span + 12, 0, IXG_TAIL_PAD + 16);
+	st->o_off = frames_tail(buf, span, hi);
+	/* the gathered offsets stay as they are (a failed launch lays the run
+	 * out again): the image gets them rebased */
+	uint64_t *o = (uint64_t *)(buf + st->o_off);
 	uint64_t lo = ~0ull;
 	for (uint32_t k = 0; k < n; k++) {
-		off[k] = (off[k] & IXG_OFF_ABS) ? (off[k] & ~IXG_OFF_ABS) : (uint64_t)(uintptr_t)buf + off[k];
-		if (off[k] < lo)
-			lo = off[k];
+		o[k] = (off[k] & IXG_OFF_ABS) ? (off[k] & ~IXG_OFF_ABS) : (uint64_t)(uintptr_t)buf + off[k];
+		if (o[k] < lo)
+			lo = o[k];
 	}
 	lo &= ~(uint64_t)15;
 	for (uint32_t k = 0; k < n; k++)
-		off[k] -= lo;
+		o[k] -= lo;
 	st->base = lo;
 	st->stride = 0;
-	st->o_off = (span + 12 + IXG_TAIL_PAD + 16 + 7) & ~(size_t)7;
-	memcpy(buf + st->o_off, off, (size_t)n * sizeof(uint64_t));
 	st->o_len = st->o_off + (size_t)n * sizeof(uint64_t);
 	memcpy(buf + st->o_len, len, (size_t)n * sizeof(uint16_t));
 	st->h2d = st->o_len + (size_t)n * sizeof(uint16_t);
 }
 
-void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint16_t *len, uint32_t n,
+void ixg_stage_finish(uint8_t *buf, size_t span, size_t hi, const uint64_t *off, const uint16_t *len, uint32_t n,
 		      struct ixg_stage *st)
 {
 	st->base = 0;
-	const size_t last_end = off[n - 1] + (len[n - 1] > 12 ? len[n - 1] : 12);
-	memset(buf + last_end, 0, IXG_TAIL_PAD + 16);
-	int uniform = 1;
-	for (uint32_t k = 1; k < n && uniform; k++)
-		uniform = len[k] == len[0];
-	const size_t frames_end = (last_end + IXG_TAIL_PAD + 16) & ~(size_t)7;
+	const size_t frames_end = frames_tail(buf, span, hi);
 	st->o_off = frames_end;
+	/* fixed stride when every frame sits at k * stride (frames staging the
+	 * same byte count; the last may differ) and none runs more than 64 bytes
+	 * past its slot (ixg_kparams.overlap) */
+	const uint64_t s = n > 1 ? off[1] - off[0] : span;
+	int uniform = off[0] == 0;
+	for (uint32_t k = 0; k < n && uniform; k++)
+		uniform = off[k] == (uint64_t)k * s && len[k] <= s + 64u;
 	if (uniform) {
-		const uint32_t l = len[0] > 12 ? len[0] : 12;
-		const uint32_t stride = (l - 12 + 3) & ~3u;
-		st->stride = stride ? stride : 4;
-		if (!stride) /* frames of <= 12 bytes: nothing staged, slots of 4 zero bytes */
+		st->stride = s ? (uint32_t)s : 4;
+		if (!s) /* frames of <= 12 bytes: nothing staged, slots of 4 zero bytes */
 			memset(buf, 0, (size_t)n * 4 + IXG_TAIL_PAD + 16);
 		st->o_len = frames_end > (size_t)n * 4 + IXG_TAIL_PAD + 16 ? frames_end : ((size_t)n * 4 + IXG_TAIL_PAD + 24) & ~(size_t)7;
 	} else {
@@ -660,7 +682,6 @@ void ixg_stage_finish(uint8_t *buf, size_t span, const uint64_t *off, const uint
 	}
 	memcpy(buf + st->o_len, len, (size_t)n * sizeof(uint16_t));
 	st->h2d = st->o_len + (size_t)n * sizeof(uint16_t);
-	(void)span;
 }
 
 /* ---- the synchronous IX-layout host path ---------------------------------- */
@@ -780,17 +801,17 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 			break;
 		/* the chunk: at most IXG_PIPE_FRAMES frames, IXG_PIPE_BYTES bytes */
 		uint32_t m = n - i < IXG_PIPE_FRAMES ? n - i : IXG_PIPE_FRAMES;
-		size_t span = 0;
+		size_t span = 0, hi = 0;
 		uint32_t done = 0;
 		while (done < m && span <= IXG_PIPE_BYTES) {
 			const uint32_t step = m - done < 256u ? m - done : 256u;
 			span = ixg_gather_mbufs(sl->h_buf, span, mbufs + i + done, step, n - i - done, sl->h_off + done,
-						sl->h_len + done);
+						sl->h_len + done, &hi);
 			done += step;
 		}
 		m = done;
 		struct ixg_stage st;
-		ixg_stage_finish(sl->h_buf, span, sl->h_off, sl->h_len, m, &st);
+		ixg_stage_finish(sl->h_buf, span, hi, sl->h_off, sl->h_len, m, &st);
 		if ((rc = ixg_stage_launch(c, &sl->ds, &st, sl->h_buf, sl->d_buf, m, sl->d_rec, sl->h_rec, 0, sl->stream)))
 			break;
 		if (hipEventRecord(sl->done, sl->stream) != hipSuccess) {

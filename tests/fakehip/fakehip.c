@@ -17,10 +17,15 @@
  * checking that every byte a kernel may read of each frame lies in memory
  * the device could reach (an allocation of this runtime or a registered
  * host range): a frame outside them would fault a real GPU, here it aborts.
+ *
+ * The runtime is thread-safe as HIP's is: one lock around every entry point
+ * (contexts on several host threads call it at once; tests/fakehip/mt_async.c
+ * runs 16 of them under ThreadSanitizer and under ASan/UBSan).
  */
 #define __HIP_PLATFORM_AMD__ 1
 #include <hip/hip_runtime_api.h>
 
+#include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -29,6 +34,10 @@
 #include "../../oracle/ixgrx_oracle.h"
 
 enum { OP_COPY, OP_SET, OP_RX, OP_MARK, OP_STAMP };
+
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
+static void lk(void) { pthread_mutex_lock(&g_mu); }
+static void ul(void) { pthread_mutex_unlock(&g_mu); }
 
 struct op {
 	int kind;
@@ -55,8 +64,8 @@ static struct ixg_rx_cfg g_cfg;
 static unsigned long g_launches;
 static int g_fail_launches;      /* the next this many RX launches fail */
 static unsigned long g_fdir_stale; /* RX launches that ran after their table changed */
-void fakehip_fail_launches(int k) { g_fail_launches = k; }
-unsigned long fakehip_fdir_stale(void) { return g_fdir_stale; }
+void fakehip_fail_launches(int k) { lk(); g_fail_launches = k; ul(); }
+unsigned long fakehip_fdir_stale(void) { lk(); unsigned long v = g_fdir_stale; ul(); return v; }
 
 /* FNV-1a over the flow-director table a launch reads (header + slots) */
 static uint64_t fdir_sum(const uint32_t *t)
@@ -78,7 +87,16 @@ static struct {
 } g_mem[MAXR];
 static int g_nmem;
 static unsigned long g_inplace; /* frames read from registered host memory */
-unsigned long fakehip_inplace_frames(void) { return g_inplace; }
+static struct ixg_kparams g_last; /* the last RX launch's parameters */
+/* the last RX launch's layout: its stride (0: u64 offsets) and frame count */
+void fakehip_last_launch(uint32_t *stride, uint32_t *n)
+{
+	lk();
+	*stride = g_last.off ? 0u : g_last.stride;
+	*n = g_last.n;
+	ul();
+}
+unsigned long fakehip_inplace_frames(void) { lk(); unsigned long v = g_inplace; ul(); return v; }
 static void mem_add(const void *p, size_t n, int registered)
 {
 	if (g_nmem == MAXR)
@@ -105,8 +123,8 @@ static int reachable(uintptr_t lo, uintptr_t hi)
 	return 0;
 }
 
-void fakehip_set_cfg(const struct ixg_rx_cfg *cfg) { g_cfg = *cfg; }
-unsigned long fakehip_launches(void) { return g_launches; }
+void fakehip_set_cfg(const struct ixg_rx_cfg *cfg) { lk(); g_cfg = *cfg; ul(); }
+unsigned long fakehip_launches(void) { lk(); unsigned long v = g_launches; ul(); return v; }
 
 static void run_op(struct op *o)
 {
@@ -188,7 +206,7 @@ static struct op *new_op(int kind)
 	return o;
 }
 
-/* ---- the runtime ---------------------------------------------------------- */
+/* ---- the runtime (every entry point under g_mu) ------------------------- */
 hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidDevice; }
 hipError_t hipGetDeviceCount(int *n)
 {
@@ -202,12 +220,19 @@ hipError_t hipGetDevicePropertiesR0600(hipDeviceProp_tR0600 *p, int d)
 	p->multiProcessorCount = 256;
 	return hipSuccess;
 }
-hipError_t hipMalloc(void **p, size_t n)
+static hipError_t dev_alloc(void **p, size_t n)
 {
 	*p = aligned_alloc(256, (n + 255) & ~(size_t)255);
 	if (*p)
 		mem_add(*p, n, 0);
 	return *p ? hipSuccess : hipErrorOutOfMemory;
+}
+hipError_t hipMalloc(void **p, size_t n)
+{
+	lk();
+	const hipError_t e = dev_alloc(p, n);
+	ul();
+	return e;
 }
 hipError_t hipHostMalloc(void **p, size_t n, unsigned int f)
 {
@@ -215,31 +240,39 @@ hipError_t hipHostMalloc(void **p, size_t n, unsigned int f)
 	return hipMalloc(p, n);
 }
 static unsigned long g_frees; /* hipFree of an allocation (a device-wide wait on HIP) */
-unsigned long fakehip_frees(void) { return g_frees; }
+unsigned long fakehip_frees(void) { lk(); unsigned long v = g_frees; ul(); return v; }
 hipError_t hipFree(void *p)
 {
+	lk();
 	g_frees += p != NULL;
 	mem_del(p);
+	ul();
 	free(p);
 	return hipSuccess;
 }
 hipError_t hipHostFree(void *p)
 {
+	lk();
 	mem_del(p);
+	ul();
 	free(p);
 	return hipSuccess;
 }
 hipError_t hipMemcpy(void *d, const void *s, size_t n, hipMemcpyKind k)
 {
 	(void)k;
+	lk();
 	drain(&g_null, NULL);
 	memcpy(d, s, n);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipMemset(void *d, int v, size_t n)
 {
+	lk();
 	drain(&g_null, NULL);
 	memset(d, v, n);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hipStream_t st)
@@ -249,7 +282,9 @@ hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hip
 	o->dst = d;
 	o->src = s;
 	o->n = n;
+	lk();
 	push(st, o);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t st)
@@ -258,7 +293,9 @@ hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t st)
 	o->dst = d;
 	o->val = v;
 	o->n = n;
+	lk();
 	push(st, o);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int f)
@@ -269,12 +306,24 @@ hipError_t hipStreamCreateWithFlags(hipStream_t *s, unsigned int f)
 }
 hipError_t hipStreamSynchronize(hipStream_t s)
 {
+	lk();
 	drain(S(s), NULL);
+	ul();
+	return hipSuccess;
+}
+/* a query runs what the stream holds (as a device that finished it by now) */
+hipError_t hipStreamQuery(hipStream_t s)
+{
+	lk();
+	drain(S(s), NULL);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipStreamDestroy(hipStream_t s)
 {
+	lk();
 	drain(S(s), NULL);
+	ul();
 	if (s)
 		free(s);
 	return hipSuccess;
@@ -295,9 +344,11 @@ hipError_t hipEventRecord(hipEvent_t e, hipStream_t st)
 	struct fevent *ev = (struct fevent *)e;
 	struct op *o = new_op(OP_MARK);
 	o->ev = ev;
+	lk();
 	ev->s = S(st);
 	ev->queried = 0;
 	push(st, o);
+	ul();
 	return hipSuccess;
 }
 /* run the event's stream up to its (latest) mark */
@@ -310,31 +361,41 @@ static void run_to(struct fevent *ev)
 }
 hipError_t hipEventSynchronize(hipEvent_t e)
 {
+	lk();
 	run_to((struct fevent *)e);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipEventQuery(hipEvent_t e)
 {
 	struct fevent *ev = (struct fevent *)e;
-	if (!ev->s)
-		return hipSuccess;
-	if (!ev->queried) {
-		ev->queried = 1;
-		return hipErrorNotReady;
+	hipError_t r = hipSuccess;
+	lk();
+	if (ev->s) {
+		if (!ev->queried) {
+			ev->queried = 1;
+			r = hipErrorNotReady;
+		} else {
+			run_to(ev);
+		}
 	}
-	run_to(ev);
-	return hipSuccess;
+	ul();
+	return r;
 }
 
 hipError_t hipHostRegister(void *p, size_t n, unsigned int f)
 {
 	(void)f;
+	lk();
 	mem_add(p, n, 1);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipHostUnregister(void *p)
 {
+	lk();
 	mem_del(p);
+	ul();
 	return hipSuccess;
 }
 hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int f)
@@ -348,26 +409,32 @@ hipError_t hipHostGetDevicePointer(void **d, void *h, unsigned int f)
 int ixgrx_launch(const void *params, uint32_t ncu, void *stream)
 {
 	(void)ncu;
+	lk();
 	if (g_fail_launches > 0) {
 		g_fail_launches--;
+		ul();
 		return -1;
 	}
 	struct op *o = new_op(OP_RX);
 	memcpy(&o->p, params, sizeof(o->p));
 	o->fdir_sum = fdir_sum(o->p.fdir);
+	g_last = o->p;
 	push((hipStream_t)stream, o);
+	ul();
 	return 0;
 }
 /* the completion stamp: written when the stream runs up to it (a poll that
  * reads the word before someone synchronizes sees the batch unfinished) */
 int ixgrx_stamp(uint32_t *flag, uint32_t v, void *stream)
 {
+	lk();
 	if (!reachable((uintptr_t)flag, (uintptr_t)(flag + 1)))
 		abort();
 	struct op *o = new_op(OP_STAMP);
 	o->dst = flag;
 	o->val = (int)v;
 	push((hipStream_t)stream, o);
+	ul();
 	return 0;
 }
 uint32_t ixgrx_kparams_size(void) { return (uint32_t)sizeof(struct ixg_kparams); }

@@ -265,3 +265,51 @@ def test_set_fdir_with_batches_in_flight():
     finally:
         eng.set_fdir(None)
         eng.close()
+
+
+def _garbage_past_ip_len(kind, n, seed):
+    """Frames whose bytes past the IP total length are random (C2's pad
+    filled; other IPv4 frames cut short of the frame at random), so a kernel
+    that read the not-staged bytes (ixg_stage_ext) would see the next frame's
+    bytes there."""
+    rng = np.random.default_rng(seed)
+    tr = traces.make_trace(kind, n, seed=seed, bad_ip=0.02, bad_l4=0.02)
+    frames = []
+    for o, L in zip(tr.offsets().astype(np.int64), tr.len.astype(np.int64)):
+        f = bytearray(tr.blob[o:o + L].tobytes())
+        if L >= 34 and f[12:14] == b"\x08\x00" and f[14] >> 4 == 4:
+            ip_len = int.from_bytes(f[16:18], "big")
+            if kind != "tcp64" and rng.random() < 0.5:
+                cut = int(rng.integers(0, max(1, min(ip_len, L - 14) - 20)))
+                ip_len -= cut
+                f[16:18] = ip_len.to_bytes(2, "big")
+            if 14 + ip_len < L:
+                f[14 + ip_len:] = rng.integers(0, 256, L - 14 - ip_len, dtype=np.uint8).tobytes()
+        frames.append(bytes(f))
+    return frames
+
+
+@pytest.mark.parametrize("kind,cfg", [
+    ("tcp64", dict(batch_frames=4096, depth=2)),               # fixed stride 44: the 6-B pads not staged
+    ("tcp64", dict(batch_frames=4096, depth=2, direct=False)),
+    ("imix", dict(batch_frames=2048, depth=4)),
+    ("mixed", dict(batch_frames=2048, depth=4)),
+])
+def test_not_staged_bytes_are_not_read(kind, cfg):
+    """the gather stages an IPv4 frame's bytes only up to
+    max(14 + ip_len, l4 + 20); the kernels, reading the image, see the next
+    frame's bytes in the rest and must give the oracle's records of the whole
+    frames."""
+    frames = _garbage_past_ip_len(kind, 30000, 71)
+    tr, arena, ptrs = _mbufs(None, 0, 0, frames=frames)
+    exp = oracle.rx_mbufs(KEY, 128, 0, 0, ptrs, threads=8)
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY))
+    try:
+        rec = eng.batch_mbufs(ptrs)
+        assert np.array_equal(rec.view(np.uint8).reshape(-1, 16), exp)
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, **cfg})
+        m, r = _run_loop(eng, ptrs, np.random.default_rng(72))
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), exp)

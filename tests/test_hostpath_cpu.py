@@ -351,3 +351,127 @@ def test_async_stats_counters(fake):
     finally:
         eng.close()
     assert np.array_equal(np.concatenate([m, m3]), ptrs[:300])
+
+
+def test_zero_copy_batch_counts_link_bytes(fake):
+    """an in-place frame costs the kernels its length in
+    host-link reads, so it counts against batch_bytes: 1514-B frames read in
+    place close a batch of 64 KiB at ~43 frames, not at batch_frames."""
+    tr, arena, ptrs = _mbufs("tcp1514", 600, seed=41)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=16384, batch_bytes=64 << 10, max_wait_us=10000000, depth=16)
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        n0 = fake.lib.fakehip_launches()
+        acc = 0
+        for k in range(0, 600, 50):
+            acc += eng.submit_mbufs(ptrs[k:k + 50])
+        eng.flush()
+        m, r = eng.poll(1000, wait=True)
+        while eng.pending():
+            m2, r2 = eng.poll(1000, wait=True)
+            m, r = np.concatenate([m, m2]), np.concatenate([r, r2])
+        st = eng.async_stats()
+        launches = fake.lib.fakehip_launches() - n0
+    finally:
+        eng.close()
+    link = 1536  # 1514 B in 64-B host-link requests
+    per = st["frames_submitted"] / max(st["batches"], 1)
+    assert acc == 600 and launches == st["batches"]
+    assert per <= (64 << 10) // link + 1, per     # closed by its link bytes
+    assert st["batches"] >= 600 * link // ((64 << 10) + link)
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+
+
+def _last_stride(lib):
+    s, n = ctypes.c_uint32(), ctypes.c_uint32()
+    lib.fakehip_last_launch(ctypes.byref(s), ctypes.byref(n))
+    return s.value, n.value
+
+
+def test_gather_stops_at_ip_len(fake):
+    """bytes past max(14 + ip_len, l4 + 20) of an IPv4
+    frame (C2's 6-B Ethernet pad) are not staged: C2 frames stage bytes
+    12..55, a 44-B stride instead of 48, and the records do not change when
+    the pads hold garbage (the gathered image then carries the next frame's
+    bytes where a frame's pad was)."""
+    rng = np.random.default_rng(42)
+    tr = traces.make_trace("tcp64", 4000, seed=43)
+    blob = tr.blob.copy()
+    offs = tr.offsets().astype(np.int64)
+    for o in offs[:, None] + np.arange(54, 60)[None, :]:
+        blob[o] = rng.integers(0, 256, o.shape, dtype=np.uint8)
+    tr = traces.Trace(blob=blob, len=tr.len, stride=tr.stride, off=tr.off)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    eng = fake()
+    try:
+        rec = eng.batch_mbufs(ptrs)
+        assert _last_stride(fake.lib) == (44, 4000)
+        eng.async_init(batch_frames=1000, batch_bytes=1 << 20, max_wait_us=10000000, depth=4)
+        m, r = _loop(eng, ptrs, rng)
+        assert _last_stride(fake.lib)[0] == 44
+    finally:
+        eng.close()
+    exp = _expect(ptrs)
+    assert np.array_equal(rec.view(np.uint8).reshape(-1, 16), exp)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), exp)
+
+
+@pytest.mark.parametrize("kind", ["imix", "mixed", "tcp1514"])
+def test_gather_garbage_past_ip_len(fake, kind):
+    """Frames whose IP total length ends short of the frame (random ip_len
+    cuts, random bytes behind them) through the shortened gather, offsets
+    layout: records as the oracle's over the whole frames."""
+    rng = np.random.default_rng(44)
+    tr = traces.make_trace(kind, 3000, seed=45)
+    frames = []
+    for o, L in zip(tr.offsets().astype(np.int64), tr.len.astype(np.int64)):
+        f = bytearray(tr.blob[o:o + L].tobytes())
+        if L >= 34 and f[12:14] == b"\x08\x00" and rng.random() < 0.5:
+            ip_len = int.from_bytes(f[16:18], "big")
+            cut = int(rng.integers(0, max(1, min(ip_len, L - 14) - 20)))
+            f[16:18] = (ip_len - cut).to_bytes(2, "big")
+            f[14 + ip_len - cut:] = rng.integers(0, 256, L - (14 + ip_len - cut), dtype=np.uint8).tobytes()
+        frames.append(bytes(f))
+    tr2 = traces.pack(frames)
+    arena, ptrs = ixgrx.make_mbufs(tr2)
+    eng = fake()
+    try:
+        rec = eng.batch_mbufs(ptrs)
+        eng.async_init(batch_frames=700, batch_bytes=1 << 18, max_wait_us=10000000, depth=3)
+        m, r = _loop(eng, ptrs, rng)
+    finally:
+        eng.close()
+    exp = _expect(ptrs)
+    assert np.array_equal(rec.view(np.uint8).reshape(-1, 16), exp)
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), exp)
+
+
+def test_zero_copy_launch_failure_retried(fake):
+    """a zero-copy batch whose launch fails is launched again
+    later; the in-place frames' offsets must be laid out again from the
+    gathered ones (the old layout step rewrote them in place, so the retry
+    rebased them twice: a GPU page fault, here fakehip's abort)."""
+    fake.lib.fakehip_inplace_frames.restype = ctypes.c_ulong
+    tr, arena, ptrs = _mbufs("tcp1514", 300, seed=46)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=128, batch_bytes=1 << 24, max_wait_us=10000000, depth=2)
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        n0 = fake.lib.fakehip_inplace_frames()
+        assert eng.submit_mbufs(ptrs[:100]) == 100
+        fake.lib.fakehip_fail_launches(1)
+        assert eng.submit_mbufs(ptrs[100:200]) == 28    # batch 1 full: its launch fails
+        with pytest.raises(RuntimeError, match="ixg_rx_poll"):
+            eng.poll(1000, wait=False)                  # the error, once
+        m, r = eng.poll(1000, wait=True)                # launched again, in place
+        while eng.pending():
+            m2, r2 = eng.poll(1000, wait=True)
+            m, r = np.concatenate([m, m2]), np.concatenate([r, r2])
+        assert fake.lib.fakehip_inplace_frames() - n0 == 128
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs[:128])
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs[:128]))

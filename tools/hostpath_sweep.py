@@ -1,7 +1,19 @@
 #!/usr/bin/env python3
-"""Sweep the asynchronous host path's knobs with examples/ix_async_loop
-(threads x batch_frames x depth x direct), 2 s per point; one JSON line per
-point (GPU box)."""
+"""Sweep the asynchronous host path with examples/ix_async_loop on the GPU
+box: one JSON line per point, with the run's cgroup CPU throttling
+(cpu.stat nr_throttled / throttled_usec deltas: the box's quota is 16 CPUs).
+
+  tools/hostpath_sweep.py SET [SECONDS]
+  SET: grid     threads x batch_frames x depth x direct (C2 frames)
+       threads  1/4/8/16 threads at the defaults (C2 frames)
+       idle     16 threads, idle=wait vs idle=spin (C2 frames)
+       big      1514-B frames at 16 threads, staged vs zero copy, batch_bytes
+                4 MiB / 1 MiB / 512 KiB / 256 KiB
+       depth    16 threads, idle=wait: depth 2/3/4 x max_wait_us 50/100
+       ab:L1,L2,..  16 threads, idle=wait, library builds interleaved over 4
+                rounds (each Li a directory holding a libixgrx.so, or
+                "default"): same-box A/B of host-path library variants
+"""
 import itertools
 import json
 import os
@@ -12,20 +24,76 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 
+def cpu_stat():
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (ln.split() for ln in f)}
+    except OSError:
+        return {}
+
+
+def point(path, label, **kw):
+    import bench
+    s0 = cpu_stat()
+    r = bench._loop_run(path, "loop", 120, batch=64, **kw)
+    s1 = cpu_stat()
+    b = r.get("breakdown", {})
+    out = {**label, "mpps": r.get("mpps"), "lat": r.get("latency_us"), "max_launch_us": b.get("max_launch_us"),
+           "max_loop_gap_us": b.get("max_loop_gap_us"), "frames_per_batch": b.get("frames_per_batch"),
+           "refused_share": b.get("refused_share"), "staged_bytes_per_frame": r.get("staged_bytes_per_frame"),
+           "throttled": s1.get("nr_throttled", 0) - s0.get("nr_throttled", 0),
+           "throttled_ms": (s1.get("throttled_usec", 0) - s0.get("throttled_usec", 0)) / 1e3, "err": r.get("error")}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     import bench
     from ix_amd import traces
-    pts = sys.argv[1] if len(sys.argv) > 1 else "default"
-    pool = traces.make_trace("tcp64", 1 << 16, seed=0x1BF000)
-    f = os.path.join(tempfile.mkdtemp(), "frames.bin")
-    bench.write_frames_file(pool, f)
-    grid = [(t, bf, dp, di) for t, bf, dp, di in itertools.product((1, 4, 8, 16), (4096, 16384), (2, 8), (0, 1))]
-    for t, bf, dp, di in grid:
-        r = bench._loop_run(f, "loop", 120, threads=t, seconds=2.0, batch=64, arena=1 << 16, cfg_frames=bf,
-                            cfg_bytes=bf * 64, cfg_depth=dp, direct=di)
-        print(json.dumps({"threads": t, "batch_frames": bf, "depth": dp, "direct": di,
-                          "mpps": r.get("mpps"), "lat_p50": r.get("latency_us", {}).get("p50"),
-                          "lat_p99": r.get("latency_us", {}).get("p99"), "err": r.get("error")}), flush=True)
+    which = sys.argv[1] if len(sys.argv) > 1 else "threads"
+    sec = float(sys.argv[2]) if len(sys.argv) > 2 else 2.0
+    tmp = tempfile.mkdtemp()
+    f = os.path.join(tmp, "frames.bin")
+    bench.write_frames_file(traces.make_trace("tcp64", 1 << 16, seed=0x1BF000), f)
+    if which == "grid":
+        for t, bf, dp, di in itertools.product((1, 4, 8, 16), (4096, 16384), (2, 8), (0, 1)):
+            point(f, dict(threads=t, batch_frames=bf, depth=dp, direct=di), threads=t, seconds=sec,
+                  arena=1 << 16, cfg_frames=bf, cfg_bytes=bf * 64, cfg_depth=dp, direct=di)
+    elif which == "threads":
+        for t in (1, 4, 8, 16):
+            point(f, dict(threads=t), threads=t, seconds=sec, arena=1 << 17)
+    elif which == "idle":
+        for idle in ("wait", "spin", "wait"):
+            point(f, dict(threads=16, idle=idle), threads=16, seconds=sec, arena=1 << 17, idle=idle)
+    elif which == "depth":
+        for dp, wu in itertools.product((2, 3, 4), (50, 100)):
+            point(f, dict(threads=16, depth=dp, max_wait_us=wu), threads=16, seconds=sec, arena=1 << 17,
+                  cfg_depth=dp, cfg_wait_us=wu)
+    elif which == "big":
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for bb in (4 << 20, 1 << 20, 512 << 10, 256 << 10):
+            for reg in (0, 1):
+                point(fb, dict(threads=16, batch_bytes=bb, zero_copy=reg), threads=16, seconds=sec,
+                      arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which.startswith("ab:"):
+        import subprocess
+        libs = which[3:].split(",")
+        for rep in range(4):
+            for lib in libs:
+                env = dict(os.environ)
+                if lib != "default":
+                    env["LD_LIBRARY_PATH"] = lib
+                s0 = cpu_stat()
+                r = subprocess.run([bench.LOOP_EXE, f, "loop", "threads=16", f"seconds={sec}", "batch=64",
+                                    f"arena={1 << 17}"], capture_output=True, text=True, timeout=120, env=env)
+                s1 = cpu_stat()
+                d = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else {}
+                print(json.dumps({"lib": lib, "rep": rep, "mpps": d.get("mpps"), "lat": d.get("latency_us"),
+                                  "max_launch_us": d.get("breakdown", {}).get("max_launch_us"),
+                                  "throttled": s1.get("nr_throttled", 0) - s0.get("nr_throttled", 0),
+                                  "rc": r.returncode}), flush=True)
+    else:
+        raise SystemExit(f"unknown set {which}")
 
 
 if __name__ == "__main__":
