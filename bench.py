@@ -326,6 +326,12 @@ def parity_leg(checks, key) -> dict:
             eext, _ = oracle.tcp_ext_batch(pool.blob, pool.off, pool.stride, er)
             ok = np.array_equal(rec, er) and np.array_equal(ext0, eext)
             res["tcpx"] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
+        elif c[0] == "icmp":
+            _, pool, rec, out, mac, host, tiled = c
+            er, _ = oracle.rx_trace(pool, key, threads=8, hash_mode=oracle.HASH_TABLE)
+            eo, k = oracle.icmp_reflect_batch(pool.blob, pool.off, 0, er, mac, host)
+            ok = np.array_equal(rec, er) and k == pool.n and np.array_equal(out[:eo.size], eo)
+            res["icmp"] = "ok" if ok and tiled else ("MISMATCH" if not ok else "MISMATCH (tiling)")
         elif c[0] == "tx":
             _, kind, (buf, segs, smac, dmacs, out, out_len), tiled = c
             size = int(segs["out_off"][-1]) + 2048
@@ -643,6 +649,65 @@ def tcpx_line(dev, steps: int, rank: int, eng_for):
             "line_floor_bytes_per_pkt": round(floor, 1),
             "frac_vs_line_floor": round(floor * wl.n / k / 1e9 / PEAK_HBM_GBPS, 4),
             "gbps_frame_bytes": round((16 + wl.stride + 16) * wl.n / k / 1e9, 1),
+            "parity": "tiled-consistent" if tiled else "MISMATCH"}, check
+
+
+def icmp_line(dev, steps: int, rank: int, eng_for, n: int = 1 << 24):
+    """ICMP echo reflect (dp/net/icmp.c:44-71,88-91) over a
+    ping flood: n default pings (56-B payload, 98-B frames, packed at
+    100-B offsets) tiled from 2^14 distinct ones in HBM, every frame an echo
+    request; the RX records come from one untimed RX launch, a step = one
+    ixg_icmp_reflect_dev launch (each lane rewrites its own frame: the lane
+    path). The parity copy is reflected once on its own buffer (a step
+    rewrites its frames in place, so the timed buffer's frames are replies
+    after the first step)."""
+    import torch
+    from ix_amd import icmp, traces
+    rng = np.random.default_rng(0x1BF200 + 97 * rank)
+    pool = traces.pack([traces.icmp_echo(rng, 56) for _ in range(1 << 14)])
+    reps = n // pool.n
+    span = int(pool.off[-1]) + 100
+    assert int(pool.len[0]) == 98 and int(pool.off[1]) == 100 and span == 100 * pool.n
+    blob = torch.from_numpy(np.ascontiguousarray(pool.blob[:span])).to(dev).repeat(reps)
+    blob = torch.cat([blob, torch.zeros(64, dtype=torch.uint8, device=dev)])
+    off = torch.arange(n, dtype=torch.int64, device=dev) * 100
+    lens = torch.full((n,), 98, dtype=torch.int16, device=dev)
+    rec = torch.empty((n, 16), dtype=torch.uint8, device=dev)
+    eng = eng_for(0)
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    eng.batch_dev(blob.data_ptr(), off.data_ptr(), lens.data_ptr(), 0, n, rec.data_ptr(), None, sp)
+    mac, host = bytes([2, 9, 8, 7, 6, 5]), 0xc0a80001
+    # the parity copy: the pool once, reflected once
+    pb = torch.from_numpy(np.ascontiguousarray(pool.blob)).to(dev)
+    icmp.reflect_dev(eng, pb.data_ptr(), off[:pool.n].data_ptr(), 0, rec.data_ptr(), pool.n, mac, host, sp)
+
+    def launch():
+        icmp.reflect_dev(eng, blob.data_ptr(), off.data_ptr(), 0, rec.data_ptr(), n, mac, host, sp)
+    for _ in range(LINE_WARMUP):
+        launch()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for a, c in ev:
+        a.record(stream)
+        launch()
+        c.record(stream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    k = float(np.mean([a.elapsed_time(c) * 1e-3 for a, c in ev]))
+    v = blob[:reps * span].view(reps, span)
+    tiled = bool(torch.equal(v, v[:1].expand(reps, -1)))
+    # algorithmic bytes per frame: the record (16), the frame bytes the reply
+    # is built from (source MAC, source IP, the 64-B message: 74) and the 23
+    # header bytes written
+    alg = 16 + 6 + 4 + 64 + 23
+    check = ("icmp", pool, rec[:pool.n].cpu().numpy(), pb.cpu().numpy(), mac, host, tiled)
+    return {"workload": f"ICMP echo reflect over a ping flood: {n} x 98-B echo requests (56-B payload) in HBM; "
+                        "kernel ixg_icmp_reflect_o",
+            "mpps": round(n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
+            "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * n / k / 1e9 / PEAK_HBM_GBPS, 4),
+            "gbps_frame_lines": round((16 + 100) * n / k / 1e9, 1),
             "parity": "tiled-consistent" if tiled else "MISMATCH"}, check
 
 
@@ -990,6 +1055,9 @@ def summary(res: dict) -> dict:
         out["tcpx"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
         if "frac_vs_line_floor" in b:
             out["tcpx"]["frac_line_floor"] = b["frac_vs_line_floor"]
+    if "icmp" in res:
+        b = res["icmp"]
+        out["icmp"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
     for kind, b in res.get("tx", {}).items():
         out["tx_" + kind] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
     hp = res.get("host_path", {})
@@ -1202,6 +1270,11 @@ def main():
         res["tcpx"], xchk = tcpx_line(dev, max(5, args.steps // 2), rank, engine)
         checks.append(xchk)
         torch.cuda.empty_cache()
+    if not args.no_demux and args.workload == "c2":
+        torch.cuda.empty_cache()
+        res["icmp"], ichk = icmp_line(dev, max(5, args.steps // 2), rank, engine)
+        checks.append(ichk)
+        torch.cuda.empty_cache()
     if not args.no_tx and args.workload == "c2":
         torch.cuda.empty_cache()
         res["tx"] = {}
@@ -1259,6 +1332,8 @@ def main():
             res["events"]["parity"] = par["events"]
         if "tcpx" in res:
             res["tcpx"]["parity"] = par["tcpx"]
+        if "icmp" in res:
+            res["icmp"]["parity"] = par["icmp"]
         if "bad_csum" in res:
             res["bad_csum"]["parity"] = par["c2b"]
     if rank == 0:

@@ -117,6 +117,10 @@ enum ixg_verdict {
 #define IXG_RF_RSS 0x10u /* rss_hash was computed (non-fragmented IPv4 TCP/UDP) */
 #define IXG_RF_FDIR 0x20u /* matched a flow-director perfect filter (ixg_rx_set_fdir): fg_id is
                              the CPU's outbound flow group, not the RSS group */
+#define IXG_RF_REPLY 0x40u /* IXG_V_ICMP_ECHO on the asynchronous path with
+                              IXG_ASYNC_ICMP_REFLECT: the mbuf already holds
+                              the echo reply icmp_input builds (icmp.c:44-71,
+                              88-91); the callee only sends it (eth_send_one) */
 
 #define IXG_NO_BUCKET 0xffffu
 
@@ -196,9 +200,16 @@ struct ixg_rx_async_cfg {
 #define IXG_ASYNC_DIRECT (1u << 0) /* the kernels read the pinned staging and
                                       write the pinned records themselves
                                       over the host link: no copies */
+#define IXG_ASYNC_ICMP_REFLECT (1u << 1) /* echo requests whose mbufs lie in a
+                                      registered region (ixg_rx_register_memory)
+                                      are turned into their replies in the
+                                      mbuf on the device, after the parse and
+                                      before poll returns them: the record
+                                      carries IXG_RF_REPLY. The reply's MAC and
+                                      address: ixg_rx_set_icmp_reply */
 #define IXG_ASYNC_MAX_DEPTH 16u
 #define IXG_ASYNC_DEF_FRAMES 16384u
-#define IXG_ASYNC_DEF_BYTES (4u << 20)
+#define IXG_ASYNC_DEF_BYTES (1u << 20)
 #define IXG_ASYNC_DEF_WAIT_US 50u
 #define IXG_ASYNC_DEF_DEPTH 2u
 #define IXG_ASYNC_DEF_FLAGS IXG_ASYNC_DIRECT
@@ -231,6 +242,14 @@ int ixg_rx_poll(void *ctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max, 
 
 /* Frames submitted and not yet returned by poll, or -errno. */
 int ixg_rx_async_pending(void *ctx);
+
+/* The source addresses of the echo replies IXG_ASYNC_ICMP_REFLECT builds:
+ * CFG.mac and CFG.host_addr (host order, as IX's cfg holds it; icmp.c:50-55).
+ * Applies to batches launched after the call. 0 or -errno. Replaces, on the
+ * asynchronous path, the per-packet icmp_reflect call of icmp_input
+ * (dp/net/icmp.c:88-92): ixg_icmp_reflect_dev's kernel over the batch's echo
+ * requests, the frames read and rewritten in their mbufs. */
+int ixg_rx_set_icmp_reply(void *ctx, const uint8_t mac[6], uint32_t host_addr);
 
 /* Where a context's asynchronous path spends its host time (cumulative since
  * ixg_rx_async_init or the last reset; for tuning IX's loop, e.g. the thread

@@ -53,6 +53,10 @@ struct ixg_abatch {
 	uint16_t *h_len;
 	void **mbufs;
 	struct ixg_rx_rec *h_rec, *d_rec;
+	/* IXG_ASYNC_ICMP_REFLECT: the echo-request candidates (pinned) */
+	uint32_t nic;
+	uint32_t *h_ic_idx;
+	uint64_t *h_ic_addr;
 };
 
 struct ixg_async {
@@ -95,6 +99,8 @@ static void batch_free(struct ixg_abatch *b)
 	hipHostFree(b->h_buf);
 	hipHostFree(b->h_done);
 	hipHostFree(b->h_rec);
+	hipHostFree(b->h_ic_idx);
+	hipHostFree(b->h_ic_addr);
 	hipFree(b->d_buf);
 	hipFree(b->d_rec);
 	free(b->h_off);
@@ -134,6 +140,10 @@ static int batch_alloc(struct ixg_async *a, struct ixg_abatch *b)
 		HIPCHK(hipMalloc((void **)&b->d_buf, bcap));
 		HIPCHK(hipMalloc((void **)&b->d_rec, (size_t)nf * sizeof(struct ixg_rx_rec)));
 	}
+	if (a->cfg.flags & IXG_ASYNC_ICMP_REFLECT) {
+		HIPCHK(hipHostMalloc((void **)&b->h_ic_idx, (size_t)nf * sizeof(uint32_t), hipHostMallocDefault));
+		HIPCHK(hipHostMalloc((void **)&b->h_ic_addr, (size_t)nf * sizeof(uint64_t), hipHostMallocDefault));
+	}
 	b->h_off = (uint64_t *)malloc((size_t)nf * sizeof(uint64_t));
 	b->h_len = (uint16_t *)malloc((size_t)nf * sizeof(uint16_t));
 	b->mbufs = (void **)malloc((size_t)nf * sizeof(void *));
@@ -154,7 +164,7 @@ int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
 		k = *cfg;
 	if (k.batch_frames == 0 || k.batch_frames > (1u << 20) || k.batch_bytes < 4096u ||
 	    k.batch_bytes > (256u << 20) || k.depth < 1 || k.depth > IXG_ASYNC_MAX_DEPTH ||
-	    (k.flags & ~(uint32_t)IXG_ASYNC_DIRECT))
+	    (k.flags & ~(uint32_t)(IXG_ASYNC_DIRECT | IXG_ASYNC_ICMP_REFLECT)))
 		return -EINVAL;
 	HIPCHK(hipSetDevice(c->device));
 	if (c->async) {
@@ -200,7 +210,9 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 		ixg_stage_finish(b->h_buf, b->span, b->hi, b->h_off, b->h_len, b->n, &st);
 	const int direct = (a->cfg.flags & IXG_ASYNC_DIRECT) != 0;
 	const uint64_t t0 = tsc();
-	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, b->stream);
+	const struct ixg_icmp_items ic = {b->nic, b->h_ic_idx, b->h_ic_addr};
+	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, &ic,
+				  b->stream);
 	if (rc == 0 && ixgrx_stamp(b->h_done, b->seq + 1u, b->stream) != 0)
 		rc = -EIO;
 	if (rc == 0)
@@ -233,7 +245,7 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
 	b->state = AS_OPEN;
 	b->t_open = t;
 	b->n = b->taken = 0;
-	b->nabs = 0;
+	b->nabs = b->nic = 0;
 	b->span = b->hi = b->link = 0;
 	a->tail = (a->tail + 1) % a->cfg.depth;
 	a->count++;
@@ -244,6 +256,29 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
  * staged ones and the in-place frames' (a zero-copy batch of 1514-B frames
  * that counted only its ~10 staged bytes per frame closed at 16384 frames,
  * 25 MB of link reads, and queued its frames for 12 ms at 16 threads) */
+/* IXG_ASYNC_ICMP_REFLECT: frames k0..k0+n-1 of batch b that may be echo
+ * requests (IPv4, protocol 1; the parse decides) and whose mbufs lie in a
+ * registered region become the batch's reflect candidates (a frame outside
+ * every region is left to the host's icmp_reflect: its record has no
+ * IXG_RF_REPLY) */
+static void icmp_candidates(const struct ixg_ctx *c, struct ixg_abatch *b, uint32_t k0, uint32_t n)
+{
+	for (uint32_t k = k0; k < k0 + n; k++) {
+		const uint8_t *mb = (const uint8_t *)b->mbufs[k];
+		const uint8_t *f = mb + IXG_MBUF_HEADER_LEN;
+		if (b->h_len[k] < 34 || f[12] != 0x08 || f[13] != 0x00 || (f[14] >> 4) != 4 || f[23] != 1)
+			continue;
+		const uintptr_t a = (uintptr_t)mb;
+		for (uint32_t r = 0; r < c->nreg; r++)
+			if (a >= c->reg[r].lo && a + IXG_MBUF_STRIDE <= c->reg[r].hi) {
+				b->h_ic_idx[b->nic] = k;
+				b->h_ic_addr[b->nic] = (uint64_t)(a + IXG_MBUF_HEADER_LEN) + (uint64_t)c->reg[r].delta;
+				b->nic++;
+				break;
+			}
+	}
+}
+
 static int due(const struct ixg_async *a, const struct ixg_abatch *b, uint64_t t)
 {
 	return b->n >= a->cfg.batch_frames || b->span + b->link >= a->cfg.batch_bytes ||
@@ -295,6 +330,8 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 				b->span = ixg_gather_mbufs(b->h_buf, b->span, mbufs + done + m, take, n - done - m,
 							   b->h_off + b->n + m, b->h_len + b->n + m, &b->hi);
 			memcpy(b->mbufs + b->n + m, mbufs + done + m, (size_t)take * sizeof(void *));
+			if ((a->cfg.flags & IXG_ASYNC_ICMP_REFLECT) && c->nreg)
+				icmp_candidates(c, b, b->n + m, take);
 			m += take;
 		}
 		a->st.gather_ns += tsc() - g0;
@@ -357,9 +394,11 @@ int ixg_async_quiesce(struct ixg_ctx *c)
  * spin, then naps that give the CPU away. On the GPU box (a cgroup quota of
  * 16 CPUs) 16 threads that spin while their rings are full, plus the HIP
  * runtime's own threads, got the whole process throttled for ~10 ms at a
- * time (cpu.stat nr_throttled 29 in 3 s). One stream query
- * per wait (not per poll) reports a failed stream early; past
- * IXG_WAIT_RUNTIME_NS the runtime's own wait decides, so a batch whose
+ * time (cpu.stat nr_throttled 29 in 3 s). The wait makes no
+ * runtime call while the batch is on time (a query per wait from 16 threads
+ * is the lock traffic the completion word removed): after
+ * IXG_WAIT_QUERY_NS one stream query reports a failed stream early, and
+ * past IXG_WAIT_RUNTIME_NS the runtime's own wait decides, so a batch whose
  * kernels failed returns -EIO instead of waiting forever. */
 #ifndef IXG_WAIT_NAP_NS
 #define IXG_WAIT_NAP_NS 10000L
@@ -372,9 +411,11 @@ int ixg_async_quiesce(struct ixg_ctx *c)
 #ifndef IXG_WAIT_SPIN
 #define IXG_WAIT_SPIN 256u
 #endif
+#define IXG_WAIT_QUERY_NS 1000000ull
 #define IXG_WAIT_RUNTIME_NS 200000000ull
 static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, int *napped)
 {
+	int queried = 0;
 	for (uint32_t k = 0;; k++) {
 		if (__atomic_load_n(b->h_done, __ATOMIC_ACQUIRE) == b->seq)
 			return 0;
@@ -384,14 +425,16 @@ static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, int *
 #endif
 			continue;
 		}
-		if (k == IXG_WAIT_SPIN) {
+		const uint64_t dt = now_ns() - t0;
+		if (!queried && dt > IXG_WAIT_QUERY_NS) {
+			queried = 1;
 			HIPCHK(hipSetDevice(c->device));
 			const hipError_t e = hipStreamQuery(b->stream);
 			if (e != hipSuccess && e != hipErrorNotReady)
 				return -EIO;
 			continue;
 		}
-		if (now_ns() - t0 > IXG_WAIT_RUNTIME_NS)
+		if (dt > IXG_WAIT_RUNTIME_NS)
 			return 1;
 		if (!*napped && IXG_WAIT_SLACK_NS > 0) {
 			*napped = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);

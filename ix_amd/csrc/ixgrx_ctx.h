@@ -42,9 +42,10 @@ struct ixg_slot {
 /* A gathered run laid out for ONE host-to-device copy (ixg_stage_finish):
  * the frames [0, frames_end) with IXG_TAIL_PAD zero bytes after the last,
  * then the u64 offsets (packed runs only), then the u16 lengths. A run
- * whose frames all have one length is a fixed-stride batch (no offsets):
- * frame k at k * stride, frames running up to 12 bytes into the next slot
- * (the skipped MAC bytes), which the launch is told (ixg_kparams.overlap). */
+ * whose frames all stage the same byte count is a fixed-stride batch (no
+ * offsets): frame k at k * stride, frames running into the next slot by the
+ * skipped MAC bytes and the bytes past ixg_stage_ext (at most 64), which the
+ * launch is told (ixg_kparams.overlap). */
 struct ixg_stage {
 	size_t h2d;          /* bytes to copy */
 	uint64_t base;       /* runs with in-place frames: the address offsets are
@@ -112,6 +113,18 @@ struct ixg_ctx {
 		intptr_t delta;
 	} reg[IXG_MAX_REGIONS];
 	uint32_t nreg;
+	/* the echo replies' source addresses (ixg_rx_set_icmp_reply) */
+	uint8_t icmp_mac[6];
+	uint32_t icmp_host;
+};
+
+/* The asynchronous path's echo-request candidates of one batch
+ * (IXG_ASYNC_ICMP_REFLECT): record index and the frame's device address in
+ * its registered mbuf, both in pinned host memory the kernel reads. */
+struct ixg_icmp_items {
+	uint32_t n;
+	const uint32_t *idx;
+	const uint64_t *addr;
 };
 
 
@@ -202,12 +215,13 @@ IXG_INTERNAL void ixg_stage_finish(uint8_t *buf, size_t span, size_t hi, const u
 IXG_INTERNAL void ixg_stage_finish_abs(uint8_t *buf, size_t span, size_t hi, const uint64_t *off,
 				      const uint16_t *len, uint32_t n, struct ixg_stage *st);
 
-/* enqueue one staged image on `s`: its H2D copy, the kernels, the D2H copy
- * of the records into h_rec; direct: the kernels read the pinned image and
- * write h_rec themselves (no copies) */
+/* enqueue one staged image on `s`: its H2D copy, the kernels, the echo
+ * reflect over `ic`'s candidates (if any), the D2H copy of the records into
+ * h_rec; direct: the kernels read the pinned image and write h_rec
+ * themselves (no copies) */
 IXG_INTERNAL int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
 		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
-		     hipStream_t s);
+		     const struct ixg_icmp_items *ic, hipStream_t s);
 
 /* ixgrx_async.c */
 IXG_INTERNAL void ixg_async_free(struct ixg_ctx *c);

@@ -757,11 +757,11 @@ static int slot_take(struct ixg_slot *sl, struct ixg_rx_rec *out)
 	return 0;
 }
 
-/* enqueue one staged image: H2D, kernels, D2H of records (the stream's
- * work; `dev_frames` is where the image is read from) */
+/* enqueue one staged image: H2D, kernels, the echo reflect over ic's
+ * candidates, D2H of records (the stream's work) */
 int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
 		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
-		     hipStream_t s)
+		     const struct ixg_icmp_items *ic, hipStream_t s)
 {
 	uint8_t *img = d_buf;
 	if (direct) {
@@ -778,6 +778,22 @@ int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_
 			       (st->stride ? IXG_LF_OVERLAP : 0u) | (direct ? IXG_LF_HOST : 0u), s);
 	if (rc)
 		return rc;
+	if (ic && ic->n) {
+		/* icmp_input's reflect (icmp.c:88-92) for the batch's echo
+		 * requests, in their mbufs, before the records are handed back */
+		struct ixg_iparams p;
+		memset(&p, 0, sizeof(p));
+		p.off = ic->addr;
+		p.idx = ic->idx;
+		p.rec = direct ? h_rec : d_rec;
+		p.n = ic->n;
+		p.mark = 1;
+		memcpy(p.mac, c->icmp_mac, 6);
+		const uint32_t be = __builtin_bswap32(c->icmp_host); /* hton32 (icmp.c:55) */
+		memcpy(p.host, &be, 4);
+		if (ixgrx_icmp_launch(&p, s) != 0)
+			return -EIO;
+	}
 	if (!direct)
 		HIPCHK(hipMemcpyAsync(h_rec, d_rec, (size_t)n * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s));
 	return 0;
@@ -812,7 +828,8 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 		m = done;
 		struct ixg_stage st;
 		ixg_stage_finish(sl->h_buf, span, hi, sl->h_off, sl->h_len, m, &st);
-		if ((rc = ixg_stage_launch(c, &sl->ds, &st, sl->h_buf, sl->d_buf, m, sl->d_rec, sl->h_rec, 0, sl->stream)))
+		if ((rc = ixg_stage_launch(c, &sl->ds, &st, sl->h_buf, sl->d_buf, m, sl->d_rec, sl->h_rec, 0, NULL,
+					   sl->stream)))
 			break;
 		if (hipEventRecord(sl->done, sl->stream) != hipSuccess) {
 			rc = -EIO;
@@ -1067,6 +1084,16 @@ int ixg_tcp_ext_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const stru
 	return ixgrx_tcpx_launch(&p, stream) == 0 ? 0 : -EIO;
 }
 
+int ixg_rx_set_icmp_reply(void *vctx, const uint8_t mac[6], uint32_t host_addr)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !mac)
+		return -EINVAL;
+	memcpy(c->icmp_mac, mac, 6);
+	c->icmp_host = host_addr;
+	return 0;
+}
+
 int ixg_icmp_reflect_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec, uint32_t n,
 			 const uint8_t mac[6], uint32_t host_addr, void *stream)
 {
@@ -1080,7 +1107,7 @@ int ixg_icmp_reflect_dev(void *vctx, const struct ixg_rx_frames *fr, const struc
 	memset(&p, 0, sizeof(p));
 	p.base = (uint8_t *)(uintptr_t)fr->base;
 	p.off = fr->off;
-	p.rec = d_rec;
+	p.rec = (struct ixg_rx_rec *)(uintptr_t)d_rec; /* read only: p.mark is 0 */
 	p.stride = fr->stride;
 	p.n = n;
 	memcpy(p.mac, mac, 6);

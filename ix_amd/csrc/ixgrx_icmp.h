@@ -15,12 +15,17 @@ extern "C" {
 struct ixg_iparams {
 	uint8_t *base;                 /* frames, rewritten in place */
 	const uint64_t *off;           /* or NULL: base + i*stride */
-	const struct ixg_rx_rec *rec;
+	struct ixg_rx_rec *rec;        /* read; with `mark`, IXG_RF_REPLY set */
+	const uint32_t *idx;           /* or NULL: item j is frame j; else the
+	                                  asynchronous path's candidate list: item
+	                                  j is record idx[j], its frame at
+	                                  base + off[j] (base NULL: off[j] is the
+	                                  frame's device address in its mbuf) */
 	uint32_t stride;
-	uint32_t n;
+	uint32_t n;                    /* items */
 	uint8_t mac[8];                /* CFG.mac (6 bytes) */
 	uint8_t host[4];               /* hton32(CFG.host_addr): the bytes written */
-	uint32_t rsvd;
+	uint32_t mark;                 /* 1: set IXG_RF_REPLY in each reflected record */
 };
 typedef struct ixg_iparams ixg_iparams;
 

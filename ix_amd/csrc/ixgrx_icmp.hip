@@ -69,9 +69,12 @@ DEV uint32_t icmp_ck(uint32_t acc, uint32_t s) {
 
 // header byte k (0..22) of the reply: Ethernet dhost = shost, shost =
 // CFG.mac (icmp.c:50-51); IP dst = src, src = CFG.host_addr (:54-55);
-// type = ICMP_ECHOREPLY (:89), checksum (:57-58). Reads before it writes.
-DEV void reply_byte(const ixg_iparams& p, uint8_t* f, uint32_t off, uint32_t ck, int k) {
-  uint32_t at, val;
+// type = ICMP_ECHOREPLY (:89), checksum (:57-58): where it goes (at) and
+// its value. Lanes 0-5 and 12-15 read bytes that lanes 6-11 and 16-19
+// write: every lane takes its value here, the wave joins a barrier, and
+// only then does any lane store (reply_store).
+DEV uint32_t reply_byte(const ixg_iparams& p, const uint8_t* f, uint32_t off, uint32_t ck, int k, uint32_t& at) {
+  uint32_t val;
   if (k < 6) {
     at = (uint32_t)k;
     val = f[6 + k];
@@ -91,7 +94,21 @@ DEV void reply_byte(const ixg_iparams& p, uint8_t* f, uint32_t off, uint32_t ck,
     at = off + 2u + (uint32_t)(k - 21);
     val = k == 21 ? (ck & 0xffu) : (ck >> 8);
   }
-  f[at] = (uint8_t)val;
+  return val;
+}
+
+// the record of item j (and where its frame is)
+template <bool OFFS>
+DEV uint8_t* item_frame(const ixg_iparams& p, uint64_t j) {
+  return reinterpret_cast<uint8_t*>(reinterpret_cast<uintptr_t>(p.base) + (OFFS ? p.off[j] : j * (uint64_t)p.stride));
+}
+DEV uint64_t item_rec(const ixg_iparams& p, uint64_t j) { return p.idx ? (uint64_t)p.idx[j] : j; }
+
+// a reflected record: IXG_RF_REPLY (the asynchronous path's candidates)
+DEV void mark_reply(const ixg_iparams& p, uint64_t r) {
+  if (!p.mark) return;
+  uint8_t* fl = reinterpret_cast<uint8_t*>(p.rec + r) + 3;
+  *fl = (uint8_t)(*fl | IXG_RF_REPLY);
 }
 
 template <bool OFFS>
@@ -101,15 +118,17 @@ DEV void reflect(const ixg_iparams& p) {
   const uint64_t i = c * 64u + (uint64_t)lane;
   bool echo = false;
   uint32_t meta = 0;  // l4_off | l4_len << 16
+  uint64_t ri = 0;    // the item's record
   if (i < p.n) {
-    const u32x2 r = reinterpret_cast<const u32x2*>(p.rec)[2u * i];
+    ri = item_rec(p, i);
+    const u32x2 r = reinterpret_cast<const u32x2*>(p.rec)[2u * ri];
     echo = ((r.x >> 16) & 0xffu) == IXG_V_ICMP_ECHO;
     meta = r.y;
   }
   // messages of at most kLaneMax bytes: each lane its own
   if (echo && (meta >> 16) <= kLaneMax) {
     const uint32_t off = meta & 0xffffu, len = meta >> 16;
-    uint8_t* f = p.base + (OFFS ? p.off[i] : i * (uint64_t)p.stride);
+    uint8_t* f = item_frame<OFFS>(p, i);
     const uintptr_t a = reinterpret_cast<uintptr_t>(f) + off;
     const uint32_t s = (uint32_t)(a & 3u);
     const uint32_t* w = reinterpret_cast<const uint32_t*>(a - s);
@@ -134,6 +153,7 @@ DEV void reflect(const ixg_iparams& p) {
     f[off] = 0u;
     f[off + 2u] = (uint8_t)(ck & 0xffu);
     f[off + 3u] = (uint8_t)(ck >> 8);
+    mark_reply(p, ri);
   }
   const bool big = echo && (meta >> 16) > kLaneMax;
   for (uint64_t m = __builtin_amdgcn_ballot_w64(big); m; m &= m - 1u) {
@@ -141,7 +161,7 @@ DEV void reflect(const ixg_iparams& p) {
     const uint64_t fi = c * 64u + (uint64_t)e;
     const uint32_t fm = __builtin_amdgcn_readlane(meta, e);
     const uint32_t off = fm & 0xffffu, len = fm >> 16;  // icmp_input's len >= 8
-    uint8_t* f = p.base + (OFFS ? p.off[fi] : fi * (uint64_t)p.stride);
+    uint8_t* f = item_frame<OFFS>(p, fi);
     // the message [a, a + len) as aligned dwords; byte k of dword j is
     // message byte 4j + k - s
     const uintptr_t a = reinterpret_cast<uintptr_t>(f) + off;
@@ -153,9 +173,14 @@ DEV void reflect(const ixg_iparams& p) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) acc = add1c(acc, (uint32_t)__shfl_xor((int)acc, d, 64));
     const uint32_t ck = icmp_ck(acc, s);  // chksum_internet, stored as is
-    // one header byte per lane (each lane reads its source byte, if any,
-    // before any lane writes: one load instruction, then one store)
-    if (lane < 23) reply_byte(p, f, off, ck, lane);
+    // one header byte per lane: all reads, a wave barrier, then the stores
+    uint32_t at = 0, val = 0;
+    if (lane < 23) val = reply_byte(p, f, off, ck, lane, at);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < 23) f[at] = (uint8_t)val;
+    if (lane == e) mark_reply(p, ri);
   }
 }
 

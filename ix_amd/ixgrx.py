@@ -41,6 +41,7 @@ VERDICTS = {
 V = {name: code for code, name in VERDICTS.items()}
 
 RF_IP_CSUM_CHECKED, RF_IP_CSUM_OK, RF_L4_CSUM_CHECKED, RF_L4_CSUM_OK, RF_RSS, RF_FDIR = 1, 2, 4, 8, 16, 32
+RF_REPLY = 64  # IXG_RF_REPLY: the asynchronous path reflected the echo request in its mbuf
 
 # symbols include/ixgrx.h declares (checked by tests/test_abi.py)
 EXPORTS = (
@@ -52,6 +53,7 @@ EXPORTS = (
     "ixg_rx_async_init", "ixg_rx_submit_mbufs", "ixg_rx_flush", "ixg_rx_poll", "ixg_rx_async_pending",
     "ixg_rx_async_stats",
     "ixg_rx_register_memory", "ixg_rx_unregister_memory", "ixg_tcp_ext_batch_dev", "ixg_icmp_reflect_dev",
+    "ixg_rx_set_icmp_reply",
 )
 
 # struct ixg_fdir_filter (12 bytes): raw IPs as in the frame, host-order ports
@@ -82,8 +84,9 @@ class AsyncStats(ctypes.Structure):
 
 
 IXG_ASYNC_DIRECT = 1 << 0
+IXG_ASYNC_ICMP_REFLECT = 1 << 1
 IXG_ZC_MIN_LEN = 256  # registered frames shorter than this are gathered anyway
-ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=4 << 20, max_wait_us=50, depth=2, direct=True)
+ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=1 << 20, max_wait_us=50, depth=2, direct=True)
 
 
 class RxFrames(ctypes.Structure):
@@ -172,6 +175,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.ixg_rx_register_memory.restype = i32
     lib.ixg_rx_unregister_memory.argtypes = [vp, vp]
     lib.ixg_rx_unregister_memory.restype = i32
+    lib.ixg_rx_set_icmp_reply.argtypes = [vp, vp, u32]
+    lib.ixg_rx_set_icmp_reply.restype = i32
     if lib.ixg_abi_version() != ABI_VERSION:
         raise RuntimeError("libixgrx ABI version mismatch")
     _libs[path] = lib
@@ -274,10 +279,17 @@ class RxEngine:
 
 
     # ---- the asynchronous host path (ixg_rx_submit_mbufs / ixg_rx_poll) ----
-    def async_init(self, batch_frames: int = 16384, batch_bytes: int = 4 << 20, max_wait_us: int = 50,
-                   depth: int = 2, direct: bool = True) -> None:
-        c = AsyncCfg(batch_frames, batch_bytes, max_wait_us, depth, IXG_ASYNC_DIRECT if direct else 0)
+    def async_init(self, batch_frames: int = 16384, batch_bytes: int = 1 << 20, max_wait_us: int = 50,
+                   depth: int = 2, direct: bool = True, icmp_reflect: bool = False) -> None:
+        flags = (IXG_ASYNC_DIRECT if direct else 0) | (IXG_ASYNC_ICMP_REFLECT if icmp_reflect else 0)
+        c = AsyncCfg(batch_frames, batch_bytes, max_wait_us, depth, flags)
         _check(self._lib.ixg_rx_async_init(self._ctx, ctypes.byref(c)), "ixg_rx_async_init", self._lib)
+
+    def set_icmp_reply(self, mac: bytes, host_addr: int) -> None:
+        """CFG.mac / CFG.host_addr of the echo replies IXG_ASYNC_ICMP_REFLECT builds."""
+        m = (ctypes.c_uint8 * 6)(*bytes(mac)[:6])
+        _check(self._lib.ixg_rx_set_icmp_reply(self._ctx, ctypes.cast(m, ctypes.c_void_p), host_addr),
+               "ixg_rx_set_icmp_reply", self._lib)
 
     def submit_mbufs(self, mbuf_ptrs: np.ndarray) -> int:
         """Frames accepted (may be fewer than given: poll, then submit the rest)."""

@@ -31,9 +31,10 @@
 
 #include "../../include/ixgrx.h"
 #include "../../ix_amd/csrc/ixgrx_internal.h"
+#include "../../ix_amd/csrc/ixgrx_icmp.h"
 #include "../../oracle/ixgrx_oracle.h"
 
-enum { OP_COPY, OP_SET, OP_RX, OP_MARK, OP_STAMP };
+enum { OP_COPY, OP_SET, OP_RX, OP_MARK, OP_STAMP, OP_ICMP };
 
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static void lk(void) { pthread_mutex_lock(&g_mu); }
@@ -46,6 +47,7 @@ struct op {
 	size_t n;
 	int val;
 	struct ixg_kparams p;
+	struct ixg_iparams ip; /* OP_ICMP */
 	uint64_t fdir_sum; /* OP_RX: the flow-director table when launched */
 	struct fevent *ev;
 	struct op *next;
@@ -88,6 +90,8 @@ static struct {
 static int g_nmem;
 static unsigned long g_inplace; /* frames read from registered host memory */
 static struct ixg_kparams g_last; /* the last RX launch's parameters */
+static unsigned long g_icmp_items; /* echo-reflect items run */
+unsigned long fakehip_icmp_items(void) { lk(); unsigned long v = g_icmp_items; ul(); return v; }
 /* the last RX launch's layout: its stride (0: u64 offsets) and frame count */
 void fakehip_last_launch(uint32_t *stride, uint32_t *n)
 {
@@ -160,6 +164,25 @@ static void run_op(struct op *o)
 	case OP_MARK:
 		o->ev->s = NULL;
 		break;
+	case OP_ICMP: {
+		/* the reflect kernel's items through the oracle, one frame each */
+		const struct ixg_iparams *q = &o->ip;
+		uint32_t host;
+		memcpy(&host, q->host, 4);
+		host = __builtin_bswap32(host);
+		for (uint32_t j = 0; j < q->n; j++) {
+			const uint64_t r = q->idx ? q->idx[j] : j;
+			uint8_t *f = (uint8_t *)((uintptr_t)q->base + (q->off ? q->off[j] : (uint64_t)j * q->stride));
+			const uint32_t len = 14u + q->rec[r].l4_off + q->rec[r].l4_len;
+			if (!reachable((uintptr_t)f, (uintptr_t)f + len) ||
+			    !reachable((uintptr_t)(q->rec + r), (uintptr_t)(q->rec + r + 1)))
+				abort();
+			if (ixgo_icmp_reflect_batch(f, NULL, 0, &q->rec[r], 1, q->mac, host) && q->mark)
+				q->rec[r].flags |= IXG_RF_REPLY;
+		}
+		g_icmp_items += q->n;
+		break;
+	}
 	case OP_STAMP:
 		__atomic_store_n((uint32_t *)o->dst, (uint32_t)o->val, __ATOMIC_RELEASE);
 		break;
@@ -456,8 +479,12 @@ int ixgrx_ev_launch(const void *p, uint32_t ncu, void *s)
 }
 int ixgrx_icmp_launch(const void *p, void *s)
 {
-	(void)p; (void)s;
-	return -1;
+	struct op *o = new_op(OP_ICMP);
+	memcpy(&o->ip, p, sizeof(o->ip));
+	lk();
+	push((hipStream_t)s, o);
+	ul();
+	return 0;
 }
 int ixgrx_tcpx_launch(const void *p, void *s)
 {

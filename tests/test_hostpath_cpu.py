@@ -475,3 +475,58 @@ def test_zero_copy_launch_failure_retried(fake):
         eng.close()
     assert np.array_equal(m, ptrs[:128])
     assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs[:128]))
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_async_icmp_reflect_golden(fake, direct):
+    """IXG_ASYNC_ICMP_REFLECT: the golden frames of the
+    reference's icmp_input (tests/golden/icmp.npz) through submit/poll with
+    the mbuf pool registered: every echo request comes back already turned
+    into the reply the reference builds in its mbuf, with IXG_RF_REPLY in
+    its record; every other frame and record is untouched."""
+    fake.lib.fakehip_icmp_items.restype = ctypes.c_ulong
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "icmp.npz")))
+    tr = traces.Trace(blob=g["blob"].copy(), off=g["off"], len=g["len"], stride=0)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    exp = _expect(ptrs)
+    refl = g["reflected"].astype(bool)
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=40, batch_bytes=1 << 20, max_wait_us=10000000, depth=3, direct=direct,
+                       icmp_reflect=True)
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        eng.set_icmp_reply(bytes(g["mac"]), int(g["host_addr"]))
+        n0 = fake.lib.fakehip_icmp_items()
+        m, r = _loop(eng, ptrs, np.random.default_rng(5), max_batch=16)
+        items = fake.lib.fakehip_icmp_items() - n0
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    got = r.view(np.uint8).reshape(-1, 16)
+    want = exp.copy()
+    want[refl, 3] |= ixgrx.RF_REPLY
+    assert np.array_equal(got, want)
+    assert items >= int(refl.sum())          # candidates: IPv4 protocol 1 frames in the region
+    base = arena.ctypes.data
+    for i, (p, o, L) in enumerate(zip(ptrs.astype(np.int64), g["off"].astype(np.int64), g["len"].astype(np.int64))):
+        mb = arena[p - base + 64:p - base + 64 + L]
+        assert np.array_equal(mb, g["after"][o:o + L]), i
+
+
+def test_async_icmp_reflect_needs_registered_mbufs(fake):
+    """Echo requests whose mbufs are not in a registered region are left to
+    the host's icmp_reflect: record unchanged (no IXG_RF_REPLY), frame
+    untouched."""
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "icmp.npz")))
+    tr = traces.Trace(blob=g["blob"].copy(), off=g["off"], len=g["len"], stride=0)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    before = arena.copy()
+    eng = fake()
+    try:
+        eng.async_init(batch_frames=64, batch_bytes=1 << 20, max_wait_us=10000000, depth=3, icmp_reflect=True)
+        eng.set_icmp_reply(bytes(g["mac"]), int(g["host_addr"]))
+        m, r = _loop(eng, ptrs, np.random.default_rng(6))
+    finally:
+        eng.close()
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+    assert np.array_equal(arena, before)

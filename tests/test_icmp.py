@@ -149,3 +149,106 @@ def test_gpu_ping_flood():
             assert np.array_equal(out, exp), f"payload {pl}"
     finally:
         eng.close()
+
+
+def _async_loop(eng, ptrs, rng, max_batch=64):
+    got_m, got_r = [], []
+    i = 0
+    while i < len(ptrs):
+        k = int(rng.integers(1, max_batch + 1))
+        acc = eng.submit_mbufs(ptrs[i:i + k])
+        i += acc
+        m, r = eng.poll(4096, wait=acc == 0)
+        got_m.append(m)
+        got_r.append(r)
+    while eng.pending():
+        m, r = eng.poll(4096, wait=True)
+        got_m.append(m)
+        got_r.append(r)
+    return np.concatenate(got_m), np.concatenate(got_r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("direct", [True, False])
+@pytest.mark.parametrize("which", ["", "2"])
+def test_gpu_async_reflect_golden(golden, which, direct):
+    """the asynchronous path with IXG_ASYNC_ICMP_REFLECT
+    and the mbuf pool registered returns the reference's echo replies
+    (icmp.npz, written by the reference's own icmp_input) already built in
+    the mbufs, with IXG_RF_REPLY in their records; other frames and records
+    as the reference's."""
+    g = golden
+    tr = traces.Trace(blob=g["blob"].copy(), off=g["off"], len=g["len"], stride=0)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    refl = g["reflected"].astype(bool)
+    eng = ixgrx.RxEngine(ixgrx.Config(bytes(g["key"])))
+    try:
+        eng.async_init(batch_frames=48, batch_bytes=1 << 20, max_wait_us=10000000, depth=3, direct=direct,
+                       icmp_reflect=True)
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        eng.set_icmp_reply(bytes(g["mac"]), int(g["host_addr" + which]))
+        m, r = _async_loop(eng, ptrs, np.random.default_rng(8), max_batch=16)
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    want = g["rec"].copy()
+    want[refl, 3] |= ixgrx.RF_REPLY
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), want)
+    base = arena.ctypes.data
+    after = g["after" + which]
+    for i, (p, o, L) in enumerate(zip(ptrs.astype(np.int64), g["off"].astype(np.int64), g["len"].astype(np.int64))):
+        assert np.array_equal(arena[p - base + 64:p - base + 64 + L], after[o:o + L]), i
+
+
+@pytest.mark.gpu
+def test_gpu_async_reflect_fuzz_vs_oracle():
+    """40K mixed frames (echo requests of every size up to 2 KiB, bad-checksum
+    requests, TCP) through submit/poll with IXG_ASYNC_ICMP_REFLECT; a third
+    of the mbufs come from an unregistered arena (left to the host's
+    icmp_reflect). Mbuf contents and records against the oracle."""
+    rng = np.random.default_rng(0x1C5)
+    n = 40000
+    frames = []
+    for i in range(n):
+        u = rng.random()
+        if u < 0.5:
+            frames.append(traces.icmp_echo(rng, int(rng.integers(0, 2048 - 42 + 1))))
+        elif u < 0.7:
+            f = bytearray(traces.icmp_echo(rng, int(rng.integers(0, 100))))
+            f[int(rng.integers(34, len(f)))] ^= 0x20
+            frames.append(bytes(f))
+        else:
+            frames.append(bytes(traces.build_ipv4(rng, 1, int(rng.choice([60, 590, 1514])), 6)[0]))
+    tr = traces.pack(frames)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    tr2 = traces.pack(frames)
+    arena2, ptrs2 = ixgrx.make_mbufs(tr2)
+    use2 = rng.random(n) < 0.33
+    mix = np.where(use2, ptrs2, ptrs)
+    key, mac, host = traces.RSS_KEY, bytes([2, 3, 5, 7, 11, 13]), 0x0a0b0c0d
+    er, _ = oracle.rx_trace(tr, key)
+    exp_frames, _ = oracle.icmp_reflect_batch(tr.blob, tr.off, 0, er, mac, host)
+    eng = ixgrx.RxEngine(ixgrx.Config(key))
+    try:
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, "icmp_reflect": True})
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        eng.set_icmp_reply(mac, host)
+        m, r = _async_loop(eng, mix, rng)
+    finally:
+        eng.close()
+    assert np.array_equal(m, mix)
+    echo = er[:, 2] == ixgrx.V["ICMP_ECHO"]
+    want = er.copy()
+    want[echo & ~use2, 3] |= ixgrx.RF_REPLY
+    got = r.view(np.uint8).reshape(-1, 16)
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} records differ, first {bad[:5]}"
+    offs, lens = tr.off.astype(np.int64), tr.len.astype(np.int64)
+    b1, b2 = arena.ctypes.data, arena2.ctypes.data
+    for i in range(n):
+        o, L = int(offs[i]), int(lens[i])
+        p = int(ptrs[i]) - b1 + 64
+        want_f = tr.blob[o:o + L] if use2[i] else exp_frames[o:o + L]
+        assert np.array_equal(arena[p:p + L], want_f), i
+        p2 = int(ptrs2[i]) - b2 + 64
+        assert np.array_equal(arena2[p2:p2 + L], tr2.blob[o:o + L]), i   # unregistered: untouched
