@@ -702,12 +702,19 @@ def icmp_line(dev, steps: int, rank: int, eng_for, n: int = 1 << 24):
     # is built from (source MAC, source IP, the 64-B message: 74) and the 23
     # header bytes written
     alg = 16 + 6 + 4 + 64 + 23
+    # what whole 128-B lines make it move: the record, every line of the
+    # frames read, every line holding a rewritten byte written back
+    o = pool.off.astype(np.int64)
+    rd = lines_touched(o + 6, o + 98)
+    wr = lines_touched(np.concatenate([o, o + 26]), np.concatenate([o + 12, o + 38]))
+    floor = 16 + (rd + wr) * 128 / pool.n
     check = ("icmp", pool, rec[:pool.n].cpu().numpy(), pb.cpu().numpy(), mac, host, tiled)
     return {"workload": f"ICMP echo reflect over a ping flood: {n} x 98-B echo requests (56-B payload) in HBM; "
                         "kernel ixg_icmp_reflect_o",
             "mpps": round(n * steps / el / 1e6, 2), "kernel_ms_avg": round(k * 1e3, 4),
             "alg_bytes_per_pkt": alg, "roofline_frac": round(alg * n / k / 1e9 / PEAK_HBM_GBPS, 4),
-            "gbps_frame_lines": round((16 + 100) * n / k / 1e9, 1),
+            "line_floor_bytes_per_pkt": round(floor, 1),
+            "frac_vs_line_floor": round(floor * n / k / 1e9 / PEAK_HBM_GBPS, 4),
             "parity": "tiled-consistent" if tiled else "MISMATCH"}, check
 
 
@@ -1058,6 +1065,8 @@ def summary(res: dict) -> dict:
     if "icmp" in res:
         b = res["icmp"]
         out["icmp"] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
+        if "frac_vs_line_floor" in b:
+            out["icmp"]["frac_line_floor"] = b["frac_vs_line_floor"]
     for kind, b in res.get("tx", {}).items():
         out["tx_" + kind] = ent(b["roofline_frac"], b["kernel_ms_avg"], b["mpps"], b["parity"])
     hp = res.get("host_path", {})

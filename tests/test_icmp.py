@@ -252,3 +252,46 @@ def test_gpu_async_reflect_fuzz_vs_oracle():
         assert np.array_equal(arena[p:p + L], want_f), i
         p2 = int(ptrs2[i]) - b2 + 64
         assert np.array_equal(arena2[p2:p2 + L], tr2.blob[o:o + L]), i   # unregistered: untouched
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["packed", "unaligned", "stride", "gaps"])
+def test_gpu_flood_span_path(layout):
+    """Waves whose 64 items are all small echo requests in increasing,
+    non-overlapping order take the span path (the wave's frames staged in LDS
+    and stored back whole): every byte of the buffer, gaps and the bytes
+    around each wave's span included, against the oracle; message lengths
+    8..128 bytes, a partial last wave, spans at every 16-byte phase."""
+    rng = np.random.default_rng(0x1C6)
+    key = traces.RSS_KEY
+    mac, host = bytes([2, 4, 6, 8, 10, 12]), 0x0a000001
+    n = 64 * 200 + 37
+    frames = [traces.icmp_echo(rng, int(rng.integers(0, 121))) for _ in range(n)]
+    if layout == "stride":
+        tr = traces.pack(frames, stride=192)
+    elif layout == "gaps":
+        # random 0..40-byte gaps of random bytes between the frames
+        gaps = rng.integers(0, 41, n)
+        off = np.zeros(n, np.uint64)
+        pos = 8
+        for i, f in enumerate(frames):
+            pos += int(gaps[i])
+            off[i] = pos
+            pos += len(f)
+        blob = rng.integers(0, 256, pos + 256, dtype=np.uint8)
+        for i, f in enumerate(frames):
+            blob[int(off[i]):int(off[i]) + len(f)] = np.frombuffer(f, np.uint8)
+        tr = traces.Trace(blob=blob, off=off, len=np.array([len(f) for f in frames], np.uint16), stride=0)
+    else:
+        tr = traces.pack(frames, align=1 if layout == "unaligned" else 4)
+    er, _ = oracle.rx_trace(tr, key)
+    assert (er[:, 2] == ixgrx.V["ICMP_ECHO"]).all()
+    exp, k = oracle.icmp_reflect_batch(tr.blob, tr.off, tr.stride or 0, er, mac, host)
+    assert k == n
+    eng = ixgrx.RxEngine(ixgrx.Config(key))
+    try:
+        out = _dev_reflect(eng, tr.blob, tr.off, tr.stride or 0, er, n, mac, host)
+    finally:
+        eng.close()
+    bad = np.nonzero(out != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
