@@ -2187,7 +2187,10 @@ DEV void short_span_body(const KParams& p) {
         if (valid) {
           const uint32_t r4 = l4_residual(st);
           const Rec r = make_record(p, d, L, st, r4);
-          store_record(p, i, r, st.ip_res, r4);
+          // non-temporal record stores: C5 0.4307 -> 0.4007 ms, c5r 0.3972
+          // -> 0.3634 ms in one process (profiles/r05/rec_nt/; the same in
+          // the long kernels: C3 1.474 -> 1.526 ms, C4 unchanged, not taken)
+          store_record<true>(p, i, r, st.ip_res, r4);
           store_demux<DMX>(p, i, r, st.src, st.dst, st.ports);
         }
       }
