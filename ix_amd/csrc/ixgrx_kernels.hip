@@ -2264,7 +2264,18 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
 // The asynchronous host path's completion stamp (ixgrx_async.c): after
 // everything enqueued before it on the stream, one lane stores v to a word of
 // coherent pinned host memory with a system-scope release, so the host sees
-// a finished batch by reading that word (no runtime call, no runtime lock)
+// a finished batch by reading that word (no runtime call, no runtime lock).
+// Ordering assumption: the batch's kernels (the RX kernels
+// writing records to pinned memory in DIRECT mode, the echo reflect writing
+// records and mbufs) and its D2H copy run before the stamp on the same
+// stream, and what they wrote is host-visible by the time the stamp is,
+// through the release fences the runtime puts on their dispatch packets and
+// copies plus this store's own system-scope release (which writes back only
+// the L2 of the XCD it runs on). HIP does not document those fence scopes;
+// what pins the assumption is the tests that read every record and every
+// reflected mbuf byte of multi-batch runs after polling the word, in DIRECT
+// and copy modes (tests/test_async.py, tests/test_icmp.py async tests,
+// tests/test_integration_example.py).
 extern "C" __global__ void __launch_bounds__(64) ixg_done_stamp(uint32_t* f, uint32_t v) {
   if (threadIdx.x == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -11,8 +11,13 @@ O=gpurun_out/$TAG
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 B="bench.py"
+# 16 hardware queues for the traced run: with the default 4, the bench's
+# 16-thread host-path loop (48 streams) crashed inside rocprofiler-sdk's
+# packet walk twice in round 5; the device lines are unchanged
+export GPU_MAX_HW_QUEUES=16
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kt" -o kt -- python3 $B \
   > "$O/bench_under_rocprof.json" 2> "$O/kt.log" || { echo "kernel-trace run failed"; tail -20 "$O/kt.log"; exit 1; }
+unset GPU_MAX_HW_QUEUES
 python3 tools/kt_summary.py "$O/kt" > "$O/launch_summary.md" || exit 1
 du -sh "$O"/* ; find "$O" -size +1M -exec ls -la {} \;
 SPECS=""
