@@ -30,7 +30,7 @@ struct mbuf {
 };
 
 struct stats {
-	unsigned tcp, udp, icmp, arp, drop;
+	unsigned tcp, udp, icmp, icmp_sent, arp, drop;
 };
 
 /* what IX's callees receive; each replaces a call made inside eth_input */
@@ -51,8 +51,13 @@ static void on_udp(void *u, void *m, const struct ixg_rx_rec *r)
 }
 static void on_icmp(void *u, void *m, const struct ixg_rx_rec *r)
 {
-	/* IX: icmp_reflect on the mbuf (icmp.c:89-92) */
-	(void)m; (void)r;
+	/* IX: with IXG_RF_REPLY (the asynchronous path with
+	 * IXG_ASYNC_ICMP_REFLECT) the mbuf already holds the reply:
+	 * eth_send_one(percpu_get(eth_num_queues)..., m, len) (icmp.c:71);
+	 * otherwise icmp_reflect on the mbuf (icmp.c:89-92) */
+	(void)m;
+	if (r->flags & IXG_RF_REPLY)
+		((struct stats *)u)->icmp_sent++;
 	((struct stats *)u)->icmp++;
 }
 static void on_arp(void *u, void *m, const struct ixg_rx_rec *r)
