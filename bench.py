@@ -801,10 +801,11 @@ def write_frames_file(tr, path: str) -> None:
             f.write(tr.blob[o:o + L].tobytes())
 
 
-def _loop_run(path: str, mode: str, timeout: float, **kw) -> dict:
+def _loop_run(path: str, mode: str, timeout: float, env: dict | None = None, **kw) -> dict:
     import subprocess
     args = [LOOP_EXE, path, mode] + [f"{k}={v}" for k, v in kw.items()]
-    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout,
+                       env=None if env is None else {**os.environ, **env})
     if r.returncode != 0:
         return {"error": f"rc={r.returncode}: {r.stderr.strip()[-300:]}"}
     return json.loads(r.stdout.strip().splitlines()[-1])

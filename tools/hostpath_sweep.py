@@ -9,6 +9,9 @@ box: one JSON line per point, with the run's cgroup CPU throttling
        idle     16 threads, idle=wait vs idle=spin (C2 frames)
        big      1514-B frames at 16 threads, staged vs zero copy, batch_bytes
                 4 MiB / 1 MiB / 512 KiB / 256 KiB
+       hwq      16 threads, GPU_MAX_HW_QUEUES 4 / 8 / 16 (the process's hardware
+                queues): C2 frames, and 1514-B frames staged / zero copy at
+                1 MiB and 512 KiB batch_bytes
        depth    16 threads, idle=wait: depth 2/3/4 x max_wait_us 50/100
        ab:L1,L2,..  16 threads, idle=wait, library builds interleaved over 4
                 rounds (each Li a directory holding a libixgrx.so, or
@@ -32,10 +35,10 @@ def cpu_stat():
         return {}
 
 
-def point(path, label, **kw):
+def point(path, label, env=None, **kw):
     import bench
     s0 = cpu_stat()
-    r = bench._loop_run(path, "loop", 120, batch=64, **kw)
+    r = bench._loop_run(path, "loop", 120, env=env, batch=64, **kw)
     s1 = cpu_stat()
     b = r.get("breakdown", {})
     out = {**label, "mpps": r.get("mpps"), "lat": r.get("latency_us"), "max_launch_us": b.get("max_launch_us"),
@@ -75,6 +78,15 @@ def main():
             for reg in (0, 1):
                 point(fb, dict(threads=16, batch_bytes=bb, zero_copy=reg), threads=16, seconds=sec,
                       arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which == "hwq":
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for rep, q in itertools.product(range(2), (4, 8, 16)):
+            env = {"GPU_MAX_HW_QUEUES": str(q)}
+            point(f, dict(hwq=q, frames=60), env=env, threads=16, seconds=sec, arena=1 << 17)
+            for bb, reg in ((1 << 20, 0), (1 << 20, 1), (512 << 10, 0), (512 << 10, 1)):
+                point(fb, dict(hwq=q, frames=1514, batch_bytes=bb, zero_copy=reg), env=env, threads=16,
+                      seconds=sec, arena=1 << 15, register=reg, cfg_bytes=bb)
     elif which.startswith("ab:"):
         import subprocess
         libs = which[3:].split(",")
