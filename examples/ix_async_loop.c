@@ -389,7 +389,7 @@ static int run_loop(void)
 	/* the per-thread breakdown, summed over threads (ns per frame of each
 	 * part of a thread's time; the rest is the loop itself and waiting) */
 	double g_ns = 0, l_ns = 0, p_ns = 0, w_ns = 0, d_s = 0, gap = 0, lmax = 0;
-	uint64_t batches = 0, by_time = 0, refused = 0, offered = 0;
+	uint64_t batches = 0, by_time = 0, refused = 0, offered = 0, img = 0, inpl = 0, launched = 0;
 	long vcs = 0, ivcs = 0;
 	for (int i = 0; i < opt.threads; i++) {
 		const struct ixg_rx_async_stats *a = &ws[i].ast;
@@ -399,6 +399,9 @@ static int run_loop(void)
 		w_ns += (double)a->wait_ns;
 		d_s += ws[i].t_dispatch;
 		batches += a->batches;
+		img += a->image_bytes;
+		inpl += a->inplace_bytes;
+		launched += a->frames_launched;
 		by_time += a->batches_by_time;
 		refused += a->frames_refused;
 		offered += a->frames_refused + a->frames_submitted;
@@ -417,30 +420,16 @@ static int run_loop(void)
 		o += ws[i].nlat;
 	}
 	qsort(lat, nl, sizeof(double), cmp_d);
-	/* bytes per frame the CPU writes into the staged image: frame bytes past
-	 * the MAC addresses (4-aligned) + the length (+ the offset, non-uniform
-	 * pools); zero copy: the offset and the length only (the kernels read
-	 * the frame in place) */
-	uint64_t staged = 0;
-	int uniform = 1;
-	for (uint32_t i = 0; i < pool_n; i++) {
-		/* the library stages bytes [12, E): E = max(14 + ip_len, l4 + 20)
-		 * for IPv4 frames, capped at L (ixgrx_ctx.h ixg_stage_ext) */
-		const uint8_t *f = pool_frame[i];
-		uint32_t e = pool_len[i];
-		if (e >= 34 && f[12] == 0x08 && f[13] == 0 && (f[14] >> 4) == 4) {
-			uint32_t x = 14u + ((uint32_t)f[16] << 8 | f[17]), h = 14u + 4u * (f[14] & 15u) + 20u;
-			x = x > h ? x : h;
-			e = x < e ? x : e;
-		}
-		staged += e > 12 ? ((e - 12u + 3u) & ~3u) : 0u;
-		uniform &= pool_len[i] == pool_len[0];
-	}
-	const double staged_b = opt.reg ? 10.0 : (double)staged / pool_n + 2.0 + (uniform ? 0.0 : 8.0);
+	/* bytes per frame of the staged images the library launched (frame bytes
+	 * past the MAC addresses up to the IP total length, 4-aligned, offsets
+	 * and lengths unless the run is of fixed stride / one length; zero copy:
+	 * offsets and lengths only, the frames are read in place) */
+	const double staged_b = launched ? (double)img / (double)launched : 0.0;
+	const double inplace_b = launched ? (double)inpl / (double)launched : 0.0;
 	printf("{\"mode\": \"loop\", \"threads\": %d, \"seconds\": %.3f, \"frames\": %llu, \"mpps\": %.2f, "
 	       "\"iterations\": %llu, \"frames_per_iteration\": %.1f, \"batch\": %d, "
 	       "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"n\": %zu}, "
-	       "\"staged_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
+	       "\"staged_bytes_per_frame\": %.1f, \"inplace_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
 	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d, "
 	       "\"zero_copy\": %d}, "
 	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}, "
@@ -450,7 +439,7 @@ static int run_loop(void)
 	       "\"max_loop_gap_us\": %.1f, \"max_launch_us\": %.1f, \"context_switches\": {\"voluntary\": %ld, \"involuntary\": %ld}}}\n",
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
-	       nl ? lat[nl - 1] : 0.0, nl, staged_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
+	       nl ? lat[nl - 1] : 0.0, nl, staged_b, inplace_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
 	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, (unsigned long long)st.tcp,
 	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
 	       (unsigned long long)st.drop, el * opt.threads * 1e9 / fr, g_ns / fr,

@@ -267,6 +267,11 @@ struct ixg_rx_async_stats {
 	uint64_t poll_ns;          /* poll: completion checks and copying records out */
 	uint64_t wait_ns;          /* poll with wait != 0: blocked on the GPU */
 	uint64_t launch_max_ns;    /* the longest single batch launch */
+	uint64_t image_bytes;      /* staged images of the launched batches: frame bytes, offsets,
+	                              lengths (what the kernels or the copies read over the link) */
+	uint64_t inplace_bytes;    /* in-place (zero-copy) frames of the launched batches, in
+	                              64-B requests */
+	uint64_t frames_launched;  /* frames of the launched batches */
 };
 /* Copy the counters to *out (may be NULL) and, reset != 0, zero them. 0 or -errno. */
 int ixg_rx_async_stats(void *ctx, struct ixg_rx_async_stats *out, int reset);

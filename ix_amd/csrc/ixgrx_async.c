@@ -212,9 +212,7 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	const uint64_t t0 = tsc();
 	const struct ixg_icmp_items ic = {b->nic, b->h_ic_idx, b->h_ic_addr};
 	int rc = ixg_stage_launch(c, &b->ds, &st, b->h_buf, b->d_buf, b->n, b->d_rec, b->h_rec, direct, &ic,
-				  b->stream);
-	if (rc == 0 && ixgrx_stamp(b->h_done, b->seq + 1u, b->stream) != 0)
-		rc = -EIO;
+				  b->h_done, b->seq + 1u, b->stream);
 	if (rc == 0)
 		b->seq++;
 	const uint64_t dt = tsc() - t0;
@@ -225,6 +223,9 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 		return rc;
 	b->state = AS_INFLIGHT;
 	a->st.batches++;
+	a->st.image_bytes += st.h2d;
+	a->st.inplace_bytes += b->link;
+	a->st.frames_launched += b->n;
 	if (b->n < a->cfg.batch_frames && b->span + b->link < a->cfg.batch_bytes)
 		a->st.batches_by_time++;
 	return 0;

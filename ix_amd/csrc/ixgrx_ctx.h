@@ -19,6 +19,8 @@ struct ixg_dstate {
 	size_t defer_cap;
 	uint32_t *d_present; /* [IXG_PRESENT_WORDS] (ixg_kparams.present) */
 	uint32_t epoch;      /* last launch's stamp */
+	uint16_t *d_lenc;    /* [64 * defer_cap] lengths of a uniform-length run, all lenc */
+	uint32_t lenc;       /* the value d_lenc holds (0: not filled) */
 };
 
 #define IXG_MAX_REGIONS 32u
@@ -52,6 +54,10 @@ struct ixg_stage {
 	                        relative to (0: the image itself) */
 	size_t o_off, o_len; /* where the offsets / lengths start in the image */
 	uint32_t stride;     /* fixed-stride run: the stride; else 0 */
+	uint32_t lmin;       /* the shortest frame's length */
+	uint32_t lconst;     /* fixed-stride run of equal lengths: the length, not
+	                        in the image (the kernels read it from
+	                        ixg_dstate.d_lenc); else 0 */
 };
 /* stage capacity: bytes the image needs for n frames of `span` gathered bytes */
 #define IXG_STAGE_BYTES(span, n) ((((span) + 12u + IXG_TAIL_PAD + 16u) & ~(size_t)7) + (size_t)(n) * 10u)
@@ -140,6 +146,13 @@ struct ixg_icmp_items {
 /* ixgrx_host.c; lflags: IXG_LF_* */
 #define IXG_LF_OVERLAP 1u /* fixed stride, frames overlap the next slot (ixg_kparams.overlap) */
 #define IXG_LF_HOST 2u    /* frames in host memory (ixg_kparams.host_mem) */
+#define IXG_LF_LONG 4u    /* every frame long: the general kernel alone, no short-kernel pass */
+/* a staged run whose frames are all at least this long goes to the general
+ * kernel alone (IXG_LF_LONG): no chunk of it can be short, so the short
+ * kernel's pass would only defer every chunk */
+#ifndef IXG_LONG_ONLY_LEN
+#define IXG_LONG_ONLY_LEN 256u
+#endif
 IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t lflags, hipStream_t s);
@@ -218,10 +231,11 @@ IXG_INTERNAL void ixg_stage_finish_abs(uint8_t *buf, size_t span, size_t hi, con
 /* enqueue one staged image on `s`: its H2D copy, the kernels, the echo
  * reflect over `ic`'s candidates (if any), the D2H copy of the records into
  * h_rec; direct: the kernels read the pinned image and write h_rec
- * themselves (no copies) */
+ * themselves (no copies). done_flag != NULL: then the completion stamp,
+ * *done_flag = done_val (coherent pinned host memory), after all of it */
 IXG_INTERNAL int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
 		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
-		     const struct ixg_icmp_items *ic, hipStream_t s);
+		     const struct ixg_icmp_items *ic, uint32_t *done_flag, uint32_t done_val, hipStream_t s);
 
 /* ixgrx_async.c */
 IXG_INTERNAL void ixg_async_free(struct ixg_ctx *c);

@@ -105,6 +105,7 @@ const char *ixg_strerror(int err)
 void ixg_dstate_free(struct ixg_dstate *ds)
 {
 	hipFree(ds->d_defer);
+	hipFree(ds->d_lenc);
 	hipFree(ds->d_present);
 	memset(ds, 0, sizeof(*ds));
 }
@@ -247,10 +248,14 @@ int ixg_dstate_reserve(struct ixg_dstate *ds, size_t nchunks)
 	 * launches too: the host paths reserve their largest batch when they
 	 * allocate (ixgrx_async.c batch_alloc, slot_init) */
 	hipFree(ds->d_defer);
+	hipFree(ds->d_lenc);
 	ds->d_defer = NULL;
+	ds->d_lenc = NULL;
 	ds->defer_cap = 0;
+	ds->lenc = 0;
 	const size_t cap = nchunks + nchunks / 4 + 64;
 	HIPCHK(hipMalloc((void **)&ds->d_defer, cap));
+	HIPCHK(hipMalloc((void **)&ds->d_lenc, cap * 64u * sizeof(uint16_t)));
 	ds->defer_cap = cap;
 	return 0;
 }
@@ -292,7 +297,7 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		p.n_listen = c->dmx_nlisten;
 	}
 	size_t nchunks = ((size_t)n + 63) / 64;
-	if (!c->force_general) {
+	if (!c->force_general && !(overlap & IXG_LF_LONG)) {
 		/* grows once per larger batch; not inside a graph capture */
 		int rc = ixg_dstate_reserve(ds, nchunks);
 		if (rc)
@@ -642,16 +647,21 @@ void ixg_stage_finish_abs(uint8_t *buf, size_t span, size_t hi, const uint64_t *
 	 * out again): the image gets them rebased */
 	uint64_t *o = (uint64_t *)(buf + st->o_off);
 	uint64_t lo = ~0ull;
+	uint32_t lmin = 0xffffu;
 	for (uint32_t k = 0; k < n; k++) {
 		o[k] = (off[k] & IXG_OFF_ABS) ? (off[k] & ~IXG_OFF_ABS) : (uint64_t)(uintptr_t)buf + off[k];
 		if (o[k] < lo)
 			lo = o[k];
+		if (len[k] < lmin)
+			lmin = len[k];
 	}
+	st->lmin = lmin;
 	lo &= ~(uint64_t)15;
 	for (uint32_t k = 0; k < n; k++)
 		o[k] -= lo;
 	st->base = lo;
 	st->stride = 0;
+	st->lconst = 0;
 	st->o_len = st->o_off + (size_t)n * sizeof(uint64_t);
 	memcpy(buf + st->o_len, len, (size_t)n * sizeof(uint16_t));
 	st->h2d = st->o_len + (size_t)n * sizeof(uint16_t);
@@ -668,8 +678,16 @@ void ixg_stage_finish(uint8_t *buf, size_t span, size_t hi, const uint64_t *off,
 	 * past its slot (ixg_kparams.overlap) */
 	const uint64_t s = n > 1 ? off[1] - off[0] : span;
 	int uniform = off[0] == 0;
-	for (uint32_t k = 0; k < n && uniform; k++)
-		uniform = off[k] == (uint64_t)k * s && len[k] <= s + 64u;
+	uint32_t lmin = 0xffffu, lmax = 0;
+	for (uint32_t k = 0; k < n; k++) {
+		uniform = uniform && off[k] == (uint64_t)k * s && len[k] <= s + 64u;
+		lmin = len[k] < lmin ? len[k] : lmin;
+		lmax = len[k] > lmax ? len[k] : lmax;
+	}
+	st->lmin = lmin;
+	/* a fixed-stride run of one length (a flood of equal frames) sends no
+	 * lengths: 2 bytes per frame less over the host link */
+	st->lconst = uniform && n && lmin == lmax ? lmin : 0u;
 	if (uniform) {
 		st->stride = s ? (uint32_t)s : 4;
 		if (!s) /* frames of <= 12 bytes: nothing staged, slots of 4 zero bytes */
@@ -679,6 +697,10 @@ void ixg_stage_finish(uint8_t *buf, size_t span, size_t hi, const uint64_t *off,
 		st->stride = 0;
 		memcpy(buf + st->o_off, off, (size_t)n * sizeof(uint64_t));
 		st->o_len = st->o_off + (size_t)n * sizeof(uint64_t);
+	}
+	if (st->lconst) {
+		st->h2d = st->o_len;
+		return;
 	}
 	memcpy(buf + st->o_len, len, (size_t)n * sizeof(uint16_t));
 	st->h2d = st->o_len + (size_t)n * sizeof(uint16_t);
@@ -761,7 +783,7 @@ static int slot_take(struct ixg_slot *sl, struct ixg_rx_rec *out)
  * candidates, D2H of records (the stream's work) */
 int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
 		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
-		     const struct ixg_icmp_items *ic, hipStream_t s)
+		     const struct ixg_icmp_items *ic, uint32_t *done_flag, uint32_t done_val, hipStream_t s)
 {
 	uint8_t *img = d_buf;
 	if (direct) {
@@ -773,9 +795,25 @@ int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_
 	}
 	/* frames: the image, or (in-place frames) offsets from st->base */
 	const uint8_t *frames = st->base ? (const uint8_t *)(uintptr_t)st->base : img;
-	int rc = ixg_launch_ds(c, ds, frames, st->stride ? NULL : (const uint64_t *)(img + st->o_off),
-			       (const uint16_t *)(img + st->o_len), st->stride, n, direct ? h_rec : d_rec, NULL, NULL,
-			       (st->stride ? IXG_LF_OVERLAP : 0u) | (direct ? IXG_LF_HOST : 0u), s);
+	const uint16_t *lens = (const uint16_t *)(img + st->o_len);
+	if (st->lconst) {
+		/* one length for the run: the lengths come from device memory,
+		 * filled (on this stream, before the kernels) when it changes */
+		int rc = ixg_dstate_reserve(ds, ((size_t)n + 63) / 64);
+		if (rc)
+			return rc;
+		if (ds->lenc != st->lconst) {
+			HIPCHK(hipMemsetD16Async((hipDeviceptr_t)ds->d_lenc, (unsigned short)st->lconst, ds->defer_cap * 64u,
+						 s));
+			ds->lenc = st->lconst;
+		}
+		lens = ds->d_lenc;
+	}
+	int rc = ixg_launch_ds(c, ds, frames, st->stride ? NULL : (const uint64_t *)(img + st->o_off), lens,
+			       st->stride, n, direct ? h_rec : d_rec, NULL, NULL,
+			       (st->stride ? IXG_LF_OVERLAP : 0u) | (direct ? IXG_LF_HOST : 0u) |
+				       (st->lmin >= IXG_LONG_ONLY_LEN && c->force_mode == IXG_MODE_AUTO ? IXG_LF_LONG : 0u),
+			       s);
 	if (rc)
 		return rc;
 	if (ic && ic->n) {
@@ -796,6 +834,8 @@ int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_
 	}
 	if (!direct)
 		HIPCHK(hipMemcpyAsync(h_rec, d_rec, (size_t)n * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s));
+	if (done_flag && ixgrx_stamp(done_flag, done_val, s) != 0)
+		return -EIO;
 	return 0;
 }
 
@@ -828,7 +868,7 @@ int ixg_rx_batch_mbufs(void *vctx, void *const *mbufs, uint32_t n, struct ixg_rx
 		m = done;
 		struct ixg_stage st;
 		ixg_stage_finish(sl->h_buf, span, hi, sl->h_off, sl->h_len, m, &st);
-		if ((rc = ixg_stage_launch(c, &sl->ds, &st, sl->h_buf, sl->d_buf, m, sl->d_rec, sl->h_rec, 0, NULL,
+		if ((rc = ixg_stage_launch(c, &sl->ds, &st, sl->h_buf, sl->d_buf, m, sl->d_rec, sl->h_rec, 0, NULL, NULL, 0,
 					   sl->stream)))
 			break;
 		if (hipEventRecord(sl->done, sl->stream) != hipSuccess) {

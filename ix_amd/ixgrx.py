@@ -80,7 +80,8 @@ class AsyncStats(ctypes.Structure):
     """struct ixg_rx_async_stats"""
     _fields_ = [(k, ctypes.c_uint64) for k in (
         "frames_submitted", "frames_returned", "frames_refused", "submit_calls", "poll_calls", "batches",
-        "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns", "launch_max_ns")]
+        "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns", "launch_max_ns",
+        "image_bytes", "inplace_bytes", "frames_launched")]
 
 
 IXG_ASYNC_DIRECT = 1 << 0

@@ -34,7 +34,7 @@
 #include "../../ix_amd/csrc/ixgrx_icmp.h"
 #include "../../oracle/ixgrx_oracle.h"
 
-enum { OP_COPY, OP_SET, OP_RX, OP_MARK, OP_STAMP, OP_ICMP };
+enum { OP_COPY, OP_SET, OP_SET16, OP_RX, OP_MARK, OP_STAMP, OP_ICMP };
 
 static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static void lk(void) { pthread_mutex_lock(&g_mu); }
@@ -91,6 +91,7 @@ static int g_nmem;
 static unsigned long g_inplace; /* frames read from registered host memory */
 static struct ixg_kparams g_last; /* the last RX launch's parameters */
 static unsigned long g_icmp_items; /* echo-reflect items run */
+static unsigned long g_stamps;     /* stamp kernels run */
 unsigned long fakehip_icmp_items(void) { lk(); unsigned long v = g_icmp_items; ul(); return v; }
 /* the last RX launch's layout: its stride (0: u64 offsets) and frame count */
 void fakehip_last_launch(uint32_t *stride, uint32_t *n)
@@ -129,6 +130,7 @@ static int reachable(uintptr_t lo, uintptr_t hi)
 
 void fakehip_set_cfg(const struct ixg_rx_cfg *cfg) { lk(); g_cfg = *cfg; ul(); }
 unsigned long fakehip_launches(void) { lk(); unsigned long v = g_launches; ul(); return v; }
+unsigned long fakehip_stamps(void) { lk(); unsigned long v = g_stamps; ul(); return v; }
 
 static void run_op(struct op *o)
 {
@@ -138,6 +140,10 @@ static void run_op(struct op *o)
 		break;
 	case OP_SET:
 		memset(o->dst, o->val, o->n);
+		break;
+	case OP_SET16:
+		for (size_t k = 0; k < o->n; k++)
+			((uint16_t *)o->dst)[k] = (uint16_t)o->val;
 		break;
 	case OP_RX: {
 		/* the bytes the kernels may read of frame i: its first max(L, 112)
@@ -185,6 +191,7 @@ static void run_op(struct op *o)
 	}
 	case OP_STAMP:
 		__atomic_store_n((uint32_t *)o->dst, (uint32_t)o->val, __ATOMIC_RELEASE);
+		g_stamps++;
 		break;
 	}
 }
@@ -313,6 +320,17 @@ hipError_t hipMemcpyAsync(void *d, const void *s, size_t n, hipMemcpyKind k, hip
 hipError_t hipMemsetAsync(void *d, int v, size_t n, hipStream_t st)
 {
 	struct op *o = new_op(OP_SET);
+	o->dst = d;
+	o->val = v;
+	o->n = n;
+	lk();
+	push(st, o);
+	ul();
+	return hipSuccess;
+}
+hipError_t hipMemsetD16Async(hipDeviceptr_t d, unsigned short v, size_t n, hipStream_t st)
+{
+	struct op *o = new_op(OP_SET16);
 	o->dst = d;
 	o->val = v;
 	o->n = n;

@@ -178,6 +178,48 @@ def test_sync_mbuf_path_skips_macs():
         assert np.array_equal(r2, r1), kind
 
 
+def _long_frames(n, seed):
+    """Frames of at least 256 B only (every batch goes to the general kernel
+    alone, IXG_LF_LONG): the IMIX 590/1514-B frames with bad checksums, cut
+    to random lengths >= 256 (ip_len then exceeds L: drops), and frames of
+    exactly 256 B."""
+    rng = np.random.default_rng(seed)
+    tr = traces.make_trace("imix", 4 * n, seed=seed, bad_ip=0.02, bad_l4=0.02)
+    big = [tr.frame(i) for i in range(tr.n) if tr.len[i] >= 256][:n]
+    out = []
+    for f in big:
+        r = rng.random()
+        if r < 0.1:
+            f = f[:int(rng.integers(256, len(f) + 1))]
+        elif r < 0.15:
+            f = f[:256]
+        out.append(f)
+    return traces.pack(out)
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_long_only_batches(register):
+    """Batches whose frames are all >= IXG_LONG_ONLY_LEN skip the short
+    kernel's pass; staged and in place, records as the oracle's."""
+    rng = np.random.default_rng(0x10F)
+    tr = _long_frames(12000, 0x10F0)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY))
+    try:
+        eng.async_init(**ixgrx.ASYNC_DEFAULTS)
+        if register:
+            eng.register_memory(arena.ctypes.data, arena.nbytes)
+        m, r = _run_loop(eng, ptrs, rng)
+        if register:
+            eng.unregister_memory(arena.ctypes.data)
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    er = oracle.rx_mbufs(KEY, 128, 0, 0, ptrs, threads=8)
+    bad = np.nonzero((r.view(np.uint8).reshape(-1, 16) != er).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} records differ, first {bad[:5]}"
+
+
 @pytest.mark.parametrize("kind", ["tcp64", "imix", "mixed", "tcp1514"])
 def test_zero_copy_registered_mbufs(kind):
     """Registered mbuf memory: the kernels read the frames in place over the

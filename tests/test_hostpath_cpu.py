@@ -135,6 +135,76 @@ def test_async_submit_poll(fake, kind, cfg):
     assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
 
 
+def test_async_uniform_length_runs(fake):
+    """Fixed-stride runs of one length send no lengths (the kernels read the
+    length from device memory, refilled on the batch's stream when it
+    changes): batches of 64 equal frames whose length changes from batch to
+    batch, a ring of 3 batches in flight, every record against the oracle;
+    the staged image is 44 B per 60-B frame."""
+    rng = np.random.default_rng(0x1E)
+    seq = [60, 62, 60, 100, 100, 58, 60, 61, 1514, 60]
+    frames = []
+    for L in seq * 4:
+        tr = traces.make_trace("tcp64", 64, seed=int(rng.integers(1 << 30)), bad_ip=0.05, bad_l4=0.05)
+        for i in range(64):
+            f = tr.frame(i)
+            frames.append(f[:L] if L <= len(f) else f + bytes(rng.integers(0, 256, L - len(f), dtype=np.uint8)))
+    arena, ptrs = ixgrx.make_mbufs(traces.pack(frames))
+    eng = fake()
+    try:
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, "batch_frames": 64, "depth": 3})
+        got_m, got_r = [], []
+        for b in range(0, len(ptrs), 64):
+            while eng.submit_mbufs(ptrs[b:b + 64]) != 64:
+                m, r = eng.poll(1000, wait=True)
+                got_m.append(m)
+                got_r.append(r)
+        while eng.pending():
+            m, r = eng.poll(1000, wait=True)
+            got_m.append(m)
+            got_r.append(r)
+        st = eng.async_stats()
+    finally:
+        eng.close()
+    assert np.array_equal(np.concatenate(got_m), ptrs)
+    assert np.array_equal(np.concatenate(got_r).view(np.uint8).reshape(-1, 16), _expect(ptrs))
+    assert st["frames_launched"] == len(ptrs) and st["inplace_bytes"] == 0
+    # C2's 60-B frames alone: [12, 56) staged, nothing else per frame
+    tr = traces.make_trace("tcp64", 4096, seed=0x1E1)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    eng = fake()
+    try:
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, "batch_frames": 4096, "max_wait_us": 1000000})
+        _loop(eng, ptrs, rng)
+        st = eng.async_stats()
+    finally:
+        eng.close()
+    assert 44.0 <= st["image_bytes"] / st["frames_launched"] < 44.5, st
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_async_one_completion_stamp_per_batch(fake, direct):
+    """Every launched batch gets exactly one completion stamp, after its
+    kernels (and, in copy mode, the records' D2H copy). Records as the
+    oracle's."""
+    lib = fake.lib
+    lib.fakehip_stamps.restype = ctypes.c_ulong
+    rng = np.random.default_rng(0x57)
+    for kind in ("tcp64", "imix", "tcp1514"):
+        tr, arena, ptrs = _mbufs(kind, 3000, seed=0x570)
+        eng = fake()
+        s0 = lib.fakehip_stamps()
+        try:
+            eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, "batch_frames": 512, "direct": direct})
+            m, r = _loop(eng, ptrs, rng)
+            st = eng.async_stats()
+        finally:
+            eng.close()
+        assert np.array_equal(m, ptrs)
+        assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+        assert lib.fakehip_stamps() - s0 == st["batches"], kind
+
+
 def test_async_aggregates_iterations(fake):
     """64-frame submissions are aggregated: 100 iterations of 64 frames with
     batch_frames 1600 make 4 launches, not 100."""

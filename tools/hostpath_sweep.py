@@ -13,11 +13,14 @@ box: one JSON line per point, with the run's cgroup CPU throttling
                 queues): C2 frames, and 1514-B frames staged / zero copy at
                 1 MiB and 512 KiB batch_bytes
        depth    16 threads, idle=wait: depth 2/3/4 x max_wait_us 50/100
-       ab:L1,L2,..  16 threads, idle=wait, library builds interleaved over 4
+       abbig:L1,L2,..  as ab, over 1514-B frames: staged and zero copy at
+                batch_bytes 1 MiB and 512 KiB
+       ab:L1,L2,..  (or L1+L2+..) 16 threads, idle=wait, library builds interleaved over 4
                 rounds (each Li a directory holding a libixgrx.so, or
                 "default"): same-box A/B of host-path library variants
 """
 import itertools
+import re
 import json
 import os
 import sys
@@ -87,9 +90,18 @@ def main():
             for bb, reg in ((1 << 20, 0), (1 << 20, 1), (512 << 10, 0), (512 << 10, 1)):
                 point(fb, dict(hwq=q, frames=1514, batch_bytes=bb, zero_copy=reg), env=env, threads=16,
                       seconds=sec, arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which.startswith("abbig:"):
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for rep in range(2):
+            for bb, reg in ((1 << 20, 0), (1 << 20, 1), (512 << 10, 0), (512 << 10, 1)):
+                for lib in re.split("[,+]", which[6:]):
+                    env = None if lib == "default" else {"LD_LIBRARY_PATH": lib}
+                    point(fb, dict(lib=lib, rep=rep, batch_bytes=bb, zero_copy=reg), env=env, threads=16,
+                          seconds=sec, arena=1 << 15, register=reg, cfg_bytes=bb)
     elif which.startswith("ab:"):
         import subprocess
-        libs = which[3:].split(",")
+        libs = re.split("[,+]", which[3:])
         for rep in range(4):
             for lib in libs:
                 env = dict(os.environ)
