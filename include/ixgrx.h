@@ -209,7 +209,7 @@ struct ixg_rx_async_cfg {
                                       address: ixg_rx_set_icmp_reply */
 #define IXG_ASYNC_MAX_DEPTH 16u
 #define IXG_ASYNC_DEF_FRAMES 16384u
-#define IXG_ASYNC_DEF_BYTES (1u << 20)
+#define IXG_ASYNC_DEF_BYTES (512u << 10)
 #define IXG_ASYNC_DEF_WAIT_US 50u
 #define IXG_ASYNC_DEF_DEPTH 2u
 #define IXG_ASYNC_DEF_FLAGS IXG_ASYNC_DIRECT

@@ -151,7 +151,7 @@ struct ixg_icmp_items {
  * kernel alone (IXG_LF_LONG): no chunk of it can be short, so the short
  * kernel's pass would only defer every chunk */
 #ifndef IXG_LONG_ONLY_LEN
-#define IXG_LONG_ONLY_LEN 256u
+#define IXG_LONG_ONLY_LEN 256u /* >= 96: the host-memory big-frame kernel reads every prefix unmasked */
 #endif
 IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,

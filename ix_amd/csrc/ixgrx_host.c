@@ -285,6 +285,7 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 	p.fdir = c->d_fdir;
 	p.overlap = overlap & 1u;
 	p.host_mem = (overlap >> 1) & 1u;
+	p.long_only = (overlap & IXG_LF_LONG) ? 1u : 0u;
 	if (dmx) {
 		p.dmx = dmx;
 		p.active_start = c->d_astart;

@@ -70,6 +70,9 @@ struct ixg_kparams {
 	uint32_t self_sample;  /* set by ixgrx_launch for the span-staged short
 	                          kernel when it runs first: it samples the
 	                          launch's mode itself and publishes it */
+	uint32_t long_only;    /* every frame is at least 256 bytes (the host's
+	                          IXG_LF_LONG): with host_mem, the host-memory
+	                          big-frame kernel takes the batch */
 };
 
 /* the flow-director table's hash (host and device agree on it) */

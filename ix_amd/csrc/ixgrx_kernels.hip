@@ -1070,10 +1070,12 @@ DEV void gen_pre_t(const KParams& p, const GDesc& g, int lane, const WaveLds& w,
 // lane then parses its prefix from LDS. A segment ending before L (IPv4
 // ip_len short of the frame) re-sums [96, seg_end) on its own (rare).
 
+// FPW: the frames a wave takes (64: a chunk; fewer: the host-memory kernel)
+template <uint32_t FPW = 64>
 DEV void big_issue(const KParams& p, const WaveLds& w, uint32_t r, int lane, Round& b) {
   const int g = lane / kG, gl = lane % kG;
   const uint32_t k = r * kRoundPk + (uint32_t)g;
-  const bool act = k < 64u;
+  const bool act = k < FPW;
   const uint32_t owner = act ? k : 0u;
   b.owner = k;
   b.end = act ? w.end[owner] : 0u;
@@ -1096,10 +1098,11 @@ DEV u32x4 mask_piece(const u32x4& v, int rem) {
                v.z & ones(rem - 8 < 0 ? 0 : rem - 8), v.w & ones(rem - 12 < 0 ? 0 : rem - 12)};
 }
 
+template <uint32_t FPW = 64>
 DEV void big_finish(const KParams& p, const WaveLds& w, int lane, Round& b) {
   const int gl = lane % kG;
   static_assert(kStreamBase == 16 * 6 && kPrefixDw == 24, "the prefix is pieces 0..5 of round slot t = 0");
-  if (gl < 6 && b.owner < 64u) {
+  if (gl < 6 && b.owner < FPW) {
     lds_u32* q = w.pre + b.owner * kPrefixDw + 4 * gl;
     q[0] = b.v[0].x; q[1] = b.v[0].y; q[2] = b.v[0].z; q[3] = b.v[0].w;
   }
@@ -1114,7 +1117,7 @@ DEV void big_finish(const KParams& p, const WaveLds& w, int lane, Round& b) {
   // frames longer than 2 KiB (not IX mbufs): the rest, synchronously
   const uint32_t more = 16u * kG * kT;
   if (wave_any(b.end > more)) {
-    const uint32_t owner = b.owner < 64u ? b.owner : 0u;
+    const uint32_t owner = b.owner < FPW ? b.owner : 0u;
     const uint64_t off = ((uint64_t)w.offhi[owner] << 32) | w.offlo[owner];
     const uint8_t* zero = p.zero + 16 * lane;
     for (uint32_t pos0 = more; wave_any(pos0 < b.end); pos0 += 16u * kG) {
@@ -1126,7 +1129,7 @@ DEV void big_finish(const KParams& p, const WaveLds& w, int lane, Round& b) {
   }
 #pragma unroll
   for (int m = 1; m < kG; m <<= 1) a = add1c(a, (uint32_t)__shfl_xor((int)a, m, kG));
-  if (gl == 0 && b.owner < 64u) w.sum[b.owner] = a;
+  if (gl == 0 && b.owner < FPW) w.sum[b.owner] = a;
 }
 
 // one's complement sum of the frame bytes [a, e) (a 16-aligned), lane-serial
@@ -1139,11 +1142,12 @@ DEV uint32_t span_sum(const KParams& p, uint64_t off, uint32_t a, uint32_t e) {
   return fold32(s);
 }
 
-template <bool OFFS, bool DMX = true>
+template <bool OFFS, bool DMX = true, uint32_t FPW = 64>
 DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane, const WaveLds& w,
                    const GDesc& g) {
-  const uint32_t i = chunk * 64u + (uint32_t)lane;
-  const bool valid = i < p.n;
+  static_assert(FPW % (2 * kRoundPk) == 0 && FPW <= 64, "whole round pairs");
+  const uint32_t i = chunk * FPW + (uint32_t)lane;
+  const bool valid = (uint32_t)lane < FPW && i < p.n;
   const uint32_t L = g.L;  // 0 past the end
   w.end[lane] = L;
   w.offlo[lane] = (uint32_t)g.off;
@@ -1151,15 +1155,15 @@ DEV void big_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t ch
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  constexpr uint32_t R = 64 / kRoundPk;
+  constexpr uint32_t R = FPW / kRoundPk;
   Round A, B;
-  big_issue(p, w, 0, lane, A);
+  big_issue<FPW>(p, w, 0, lane, A);
 #pragma clang loop unroll(disable)
   for (uint32_t r = 0; r < R; r += 2) {
-    big_issue(p, w, r + 1, lane, B);
-    big_finish(p, w, lane, A);
-    big_issue(p, w, r + 2, lane, A);
-    big_finish(p, w, lane, B);
+    big_issue<FPW>(p, w, r + 1, lane, B);
+    big_finish<FPW>(p, w, lane, A);
+    big_issue<FPW>(p, w, r + 2, lane, A);
+    big_finish<FPW>(p, w, lane, B);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1334,6 +1338,48 @@ DEV void stage_tables(const KParams& p, uint64_t* T) {
   }
   __syncthreads();
 }
+
+// ---- frames in host memory, all long ---------------------------------------
+// A batch in host memory (the asynchronous path's DIRECT mode) whose frames
+// are all at least kBigMin bytes (KParams.long_only): every load crosses the
+// host link, so a wave's time is its round trips, not its bytes. A 64-frame
+// chunk per wave is 16 rounds of 4 frames (8 round trips with two rounds in
+// flight): a 1514-B batch took 28-34 us per launch whether it held 342 or
+// 683 frames. Here a wave takes kHostFpw frames (kHostFpw / 4 rounds), so a
+// batch spreads over 64 / kHostFpw times the waves and has that many more
+// bytes in flight; the per-frame work (big_chunk) is the same.
+#ifndef IXG_HOST_FPW
+#define IXG_HOST_FPW 8
+#endif
+constexpr uint32_t kHostFpw = IXG_HOST_FPW;
+
+template <bool OFFS>
+DEV void host_big_body(const KParams& p) {
+  __shared__ uint64_t T[12 * 256];
+  __shared__ uint32_t sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64], sh_sum[kWaves][64];
+  __shared__ uint32_t sh_pre[kWaves][64 * kPrefixDw];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  extern __shared__ u32x4 dyn6[];
+  if (p.tab6) {
+    for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kWaves) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
+  }
+  stage_tables(p, T);
+  const WaveLds w{nullptr, LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]), LDS(lds_u32, sh_offhi[wave]),
+                  LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6), LDS(lds_u32, sh_pre[wave])};
+  const uint32_t nsub = (p.n + kHostFpw - 1u) / kHostFpw;
+  for (uint32_t c = blockIdx.x * kWaves + (uint32_t)wave; c < nsub; c += gridDim.x * kWaves) {
+    const uint32_t i = c * kHostFpw + (uint32_t)lane;
+    const bool valid = (uint32_t)lane < kHostFpw && i < p.n;
+    const uint32_t ic = valid ? i : 0u;
+    GDesc g;
+    g.L = valid ? (uint32_t)p.len[ic] : 0u;
+    g.off = frame_off<OFFS>(p, ic);
+    big_chunk<OFFS, false, kHostFpw>(p, T, c, lane, w, g);
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_host_big_s(KParams p) { host_big_body<false>(p); }
+extern "C" __global__ void __launch_bounds__(kBlock) ixg_rx_host_big_o(KParams p) { host_big_body<true>(p); }
 
 // ---- fixed-shape kernel --------------------------------------------------
 // Software-pipelined over the wave's chunks (64 packets each, grid-stride):
@@ -2295,6 +2341,15 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
   const KParams& p = *static_cast<const KParams*>(params);
   const int lay = p.off ? 1 : 0;
   const uint64_t nchunks = ((uint64_t)p.n + 63u) / 64u;
+  if (p.long_only && p.host_mem) {
+    // host-memory batch of long frames: kHostFpw frames per wave
+    static const kern_fn k_hb[2] = {ixg_rx_host_big_s, ixg_rx_host_big_o};
+    const uint64_t nsub = ((uint64_t)p.n + kHostFpw - 1u) / kHostFpw;
+    const size_t sh6 = p.tab6 ? IXG_TAB6_WORDS * sizeof(uint32_t) : 0u;
+    hipLaunchKernelGGL(k_hb[lay], dim3(grid_for(k_hb[lay], (nsub + kWaves - 1) / kWaves, ncu, sh6)), dim3(kBlock), sh6,
+                       (hipStream_t)stream, p);
+    return (int)hipGetLastError();
+  }
   const uint64_t wave_blocks = (nchunks + kWaves - 1) / kWaves;              // one wave per chunk
   const uint64_t group_blocks = ((nchunks + 63u) / 64u + kWaves - 1) / kWaves; // one wave per 64 chunks
   const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&

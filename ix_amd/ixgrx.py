@@ -87,7 +87,7 @@ class AsyncStats(ctypes.Structure):
 IXG_ASYNC_DIRECT = 1 << 0
 IXG_ASYNC_ICMP_REFLECT = 1 << 1
 IXG_ZC_MIN_LEN = 256  # registered frames shorter than this are gathered anyway
-ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=1 << 20, max_wait_us=50, depth=2, direct=True)
+ASYNC_DEFAULTS = dict(batch_frames=16384, batch_bytes=512 << 10, max_wait_us=50, depth=2, direct=True)
 
 
 class RxFrames(ctypes.Structure):
@@ -280,7 +280,7 @@ class RxEngine:
 
 
     # ---- the asynchronous host path (ixg_rx_submit_mbufs / ixg_rx_poll) ----
-    def async_init(self, batch_frames: int = 16384, batch_bytes: int = 1 << 20, max_wait_us: int = 50,
+    def async_init(self, batch_frames: int = 16384, batch_bytes: int = 512 << 10, max_wait_us: int = 50,
                    depth: int = 2, direct: bool = True, icmp_reflect: bool = False) -> None:
         flags = (IXG_ASYNC_DIRECT if direct else 0) | (IXG_ASYNC_ICMP_REFLECT if icmp_reflect else 0)
         c = AsyncCfg(batch_frames, batch_bytes, max_wait_us, depth, flags)

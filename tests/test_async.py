@@ -197,14 +197,40 @@ def _long_frames(n, seed):
     return traces.pack(out)
 
 
-@pytest.mark.parametrize("register", [False, True])
-def test_long_only_batches(register):
-    """Batches whose frames are all >= IXG_LONG_ONLY_LEN skip the short
-    kernel's pass; staged and in place, records as the oracle's."""
-    rng = np.random.default_rng(0x10F)
-    tr = _long_frames(12000, 0x10F0)
+def _long_mixed_frames(n, seed):
+    """Long frames of every header shape: IPv4 ihl 5..15 and IPv6, TCP and
+    UDP, 256..1514 B, some with bad checksums, some padded past the IP total
+    length (the segment ends before L)."""
+    rng = np.random.default_rng(seed)
+    rows = []
+    for ihl in (5, 6, 9, 15):
+        for proto in (6, 17):
+            for L in (256, 300, 590, 1514):
+                f = traces.build_ipv4(rng, 16, L, proto, ihl=ihl)
+                traces.corrupt(rng, f, 0.1, 0.1, 14 + 4 * ihl + (16 if proto == 6 else 6))
+                rows += [bytes(x) for x in f]
+    for proto in (6, 17):
+        for L in (256, 1514):
+            rows += [bytes(x) for x in traces.build_ipv6(rng, 16, L, proto)]
+    out = []
+    for k in rng.integers(0, len(rows), n):
+        f = rows[k]
+        if rng.random() < 0.1:  # padded: bytes past the IP total length
+            f = f + bytes(rng.integers(0, 256, int(rng.integers(1, 200)), dtype=np.uint8))
+        out.append(f)
+    return traces.pack(out)
+
+
+@pytest.mark.parametrize("register,flags", [(False, 0), (True, 0), (False, ixgrx.IXG_F_IPV6),
+                                            (True, ixgrx.IXG_F_IPV6)])
+def test_long_only_batches(register, flags):
+    """Batches whose frames are all >= IXG_LONG_ONLY_LEN go to the
+    host-memory big-frame kernel (DIRECT: a few frames per wave); staged and
+    in place, every header shape, records as the oracle's."""
+    rng = np.random.default_rng(0x10F + flags)
+    tr = _long_frames(6000, 0x10F0) if not flags else _long_mixed_frames(6000, 0x10F1)
     arena, ptrs = ixgrx.make_mbufs(tr)
-    eng = ixgrx.RxEngine(ixgrx.Config(KEY))
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY, 128, 0, flags))
     try:
         eng.async_init(**ixgrx.ASYNC_DEFAULTS)
         if register:
@@ -215,7 +241,7 @@ def test_long_only_batches(register):
     finally:
         eng.close()
     assert np.array_equal(m, ptrs)
-    er = oracle.rx_mbufs(KEY, 128, 0, 0, ptrs, threads=8)
+    er = oracle.rx_mbufs(KEY, 128, 0, flags, ptrs, threads=8)
     bad = np.nonzero((r.view(np.uint8).reshape(-1, 16) != er).any(axis=1))[0]
     assert bad.size == 0, f"{bad.size} records differ, first {bad[:5]}"
 

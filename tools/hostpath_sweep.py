@@ -9,6 +9,8 @@ box: one JSON line per point, with the run's cgroup CPU throttling
        idle     16 threads, idle=wait vs idle=spin (C2 frames)
        big      1514-B frames at 16 threads, staged vs zero copy, batch_bytes
                 4 MiB / 1 MiB / 512 KiB / 256 KiB
+       bigbytes 1514-B frames at 16 threads, staged and zero copy, batch_bytes
+                512 / 640 / 768 / 1024 KiB, three rounds
        hwq      16 threads, GPU_MAX_HW_QUEUES 4 / 8 / 16 (the process's hardware
                 queues): C2 frames, and 1514-B frames staged / zero copy at
                 1 MiB and 512 KiB batch_bytes
@@ -81,6 +83,14 @@ def main():
             for reg in (0, 1):
                 point(fb, dict(threads=16, batch_bytes=bb, zero_copy=reg), threads=16, seconds=sec,
                       arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which == "bigbytes":
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for rep in range(3):
+            for bb in (512 << 10, 640 << 10, 768 << 10, 1 << 20):
+                for reg in (0, 1):
+                    point(fb, dict(rep=rep, batch_bytes=bb, zero_copy=reg), threads=16, seconds=sec,
+                          arena=1 << 15, register=reg, cfg_bytes=bb)
     elif which == "hwq":
         fb = os.path.join(tmp, "frames1514.bin")
         bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
