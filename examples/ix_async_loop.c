@@ -24,6 +24,9 @@
  *   cfg_frames= cfg_bytes= cfg_wait_us= cfg_depth= direct=0|1 dump=FILE
  *   register=1: register each thread's mbuf arena (ixg_rx_register_memory)
  *   so the kernels read the frames in place (zero copy)
+ *   pages=huge|4k: the mbuf arenas on 2 MB pages as IX's mempools are
+ *   (dp/core/mempool.c:198-243: hugetlbfs pages if the host has them
+ *   reserved, else transparent huge pages; the default), or on 4 KB pages
  *   idle=wait|spin: an iteration whose frames the full ring refused either
  *   waits in ixg_rx_poll for the oldest batch (wait, the default: the CPU
  *   has no RX work until a batch returns, and gives its time away) or polls
@@ -41,6 +44,7 @@
 #include <ucontext.h>
 #include <signal.h>
 #include <unistd.h>
+#include <sys/mman.h>
 #include <sys/resource.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -108,11 +112,11 @@ static void install_fault_dump(void)
 /* ---- options ------------------------------------------------------------- */
 static struct {
 	const char *frames, *mode, *dump;
-	int threads, batch, device, direct, reg, spin;
+	int threads, batch, device, direct, reg, spin, small_pages;
 	double seconds;
 	uint32_t n, arena;
 	struct ixg_rx_async_cfg acfg;
-} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 0, 2.0, 64, 1u << 16,
+} opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 0, 0, 2.0, 64, 1u << 16,
 	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}};
 
 static const uint8_t rss_key[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
@@ -150,10 +154,37 @@ static int load_pool(const char *path)
 
 /* an arena of n IX mbufs holding the pool tiled: len = size_t at +0, data at
  * +64 (inc/ix/mbuf.h:73-90) */
+#define HUGE_PAGE (2u << 20)
+static const char *arena_pages = "4k"; /* what the arenas got: hugetlb, thp or 4k */
+
+/* (+ the tail bytes the kernels may read past the last frame) */
+static size_t arena_bytes(uint32_t n)
+{
+	return ((size_t)n * MBUF_STRIDE + IXG_TAIL_PAD + HUGE_PAGE - 1) & ~((size_t)HUGE_PAGE - 1);
+}
+
+static uint8_t *arena_alloc(size_t sz)
+{
+	if (opt.small_pages)
+		return aligned_alloc(4096, sz);
+	void *a = mmap(NULL, sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_HUGETLB, -1, 0);
+	if (a != MAP_FAILED) {
+		arena_pages = "hugetlb";
+		return a;
+	}
+	/* no reserved huge pages: 2 MB-aligned, transparent huge pages asked for */
+	a = mmap(NULL, sz + HUGE_PAGE, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+	if (a == MAP_FAILED)
+		return NULL;
+	uint8_t *b = (uint8_t *)(((uintptr_t)a + HUGE_PAGE - 1) & ~(uintptr_t)(HUGE_PAGE - 1));
+	if (madvise(b, sz, MADV_HUGEPAGE) == 0)
+		arena_pages = "thp";
+	return b;
+}
+
 static void **make_arena(uint32_t n, uint8_t **mem)
 {
-	/* (+ the tail bytes the kernels may read past the last frame) */
-	uint8_t *a = aligned_alloc(4096, ((size_t)n * MBUF_STRIDE + IXG_TAIL_PAD + 4095) & ~(size_t)4095);
+	uint8_t *a = arena_alloc(arena_bytes(n));
 	void **p = malloc((size_t)n * sizeof(void *));
 	if (!a || !p)
 		return NULL;
@@ -343,8 +374,7 @@ static int run_loop(void)
 		w->ptrs = make_arena(opt.arena, &w->mem);
 		if (!w->ptrs)
 			return 1;
-		if (opt.reg && (w->rc = ixg_rx_register_memory(w->ctx, w->mem,
-				      ((size_t)opt.arena * MBUF_STRIDE + IXG_TAIL_PAD + 4095) & ~(size_t)4095))) {
+		if (opt.reg && (w->rc = ixg_rx_register_memory(w->ctx, w->mem, arena_bytes(opt.arena)))) {
 			fprintf(stderr, "register %d: %s\n", i, ixg_strerror(w->rc));
 			return 2;
 		}
@@ -431,7 +461,7 @@ static int run_loop(void)
 	       "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"n\": %zu}, "
 	       "\"staged_bytes_per_frame\": %.1f, \"inplace_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
 	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d, "
-	       "\"zero_copy\": %d}, "
+	       "\"zero_copy\": %d, \"arena_pages\": \"%s\"}, "
 	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}, "
 	       "\"breakdown\": {\"thread_ns_per_frame\": %.2f, \"gather_ns_per_frame\": %.2f, \"launch_us_per_batch\": %.2f, "
 	       "\"poll_ns_per_frame\": %.2f, \"wait_ns_per_frame\": %.2f, \"dispatch_ns_per_frame\": %.2f, "
@@ -440,7 +470,7 @@ static int run_loop(void)
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
 	       nl ? lat[nl - 1] : 0.0, nl, staged_b, inplace_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
-	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, (unsigned long long)st.tcp,
+	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, arena_pages, (unsigned long long)st.tcp,
 	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
 	       (unsigned long long)st.drop, el * opt.threads * 1e9 / fr, g_ns / fr,
 	       batches ? l_ns / (double)batches / 1e3 : 0.0, p_ns / fr, w_ns / fr, d_s * 1e9 / fr,
@@ -454,7 +484,8 @@ static int run_loop(void)
 	}
 	for (int i = 0; i < opt.threads; i++) {
 		ixg_rx_fini(ws[i].ctx);
-		free(ws[i].mem);
+		if (opt.small_pages)
+			free(ws[i].mem); /* (the mapped arenas go with the process) */
 		free(ws[i].ptrs);
 		free(ws[i].lat);
 		free(ws[i].dump);
@@ -530,7 +561,8 @@ static int run_latency(int async)
 	       async ? "async1" : "sync", n, nl, mean, pct(lat, nl, 0.5), pct(lat, nl, 0.99), nl ? lat[0] : 0.0,
 	       (double)n * (double)nl / tot / 1e6, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0);
 	ixg_rx_fini(ctx);
-	free(mem);
+	if (opt.small_pages)
+		free(mem);
 	free(ptrs);
 	free(recs);
 	free(pm);
@@ -566,6 +598,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(k, "cfg_depth")) opt.acfg.depth = (uint32_t)atoi(v);
 		else if (!strcmp(k, "direct")) opt.acfg.flags = atoi(v) ? IXG_ASYNC_DIRECT : 0;
 		else if (!strcmp(k, "register")) opt.reg = atoi(v);
+		else if (!strcmp(k, "pages")) opt.small_pages = !strcmp(v, "4k");
 		else if (!strcmp(k, "idle")) opt.spin = !strcmp(v, "spin");
 		else {
 			fprintf(stderr, "unknown option %s\n", k);

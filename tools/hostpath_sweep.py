@@ -11,6 +11,8 @@ box: one JSON line per point, with the run's cgroup CPU throttling
                 4 MiB / 1 MiB / 512 KiB / 256 KiB
        bigbytes 1514-B frames at 16 threads, staged and zero copy, batch_bytes
                 512 / 640 / 768 / 1024 KiB, three rounds
+       pages    1514-B frames at 16 threads, staged and zero copy, mbuf arenas
+                on 2 MB pages (the default, as IX's mempools) vs 4 KB pages
        hwq      16 threads, GPU_MAX_HW_QUEUES 4 / 8 / 16 (the process's hardware
                 queues): C2 frames, and 1514-B frames staged / zero copy at
                 1 MiB and 512 KiB batch_bytes
@@ -49,6 +51,7 @@ def point(path, label, env=None, **kw):
     out = {**label, "mpps": r.get("mpps"), "lat": r.get("latency_us"), "max_launch_us": b.get("max_launch_us"),
            "max_loop_gap_us": b.get("max_loop_gap_us"), "frames_per_batch": b.get("frames_per_batch"),
            "refused_share": b.get("refused_share"), "staged_bytes_per_frame": r.get("staged_bytes_per_frame"),
+           "arena_pages": r.get("cfg", {}).get("arena_pages"),
            "throttled": s1.get("nr_throttled", 0) - s0.get("nr_throttled", 0),
            "throttled_ms": (s1.get("throttled_usec", 0) - s0.get("throttled_usec", 0)) / 1e3, "err": r.get("error")}
     print(json.dumps(out), flush=True)
@@ -91,6 +94,14 @@ def main():
                 for reg in (0, 1):
                     point(fb, dict(rep=rep, batch_bytes=bb, zero_copy=reg), threads=16, seconds=sec,
                           arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which == "pages":
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for rep in range(3):
+            for pages in ("huge", "4k"):
+                for reg in (0, 1):
+                    point(fb, dict(rep=rep, pages=pages, zero_copy=reg), threads=16, seconds=sec,
+                          arena=1 << 15, register=reg, pages=pages)
     elif which == "hwq":
         fb = os.path.join(tmp, "frames1514.bin")
         bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
