@@ -101,6 +101,16 @@ void fakehip_last_launch(uint32_t *stride, uint32_t *n)
 	*n = g_last.n;
 	ul();
 }
+/* the last launch's plan inputs: frames in host memory, every frame long
+ * (the host-memory big-frame kernel), deferral in use */
+void fakehip_last_plan(uint32_t *host_mem, uint32_t *long_only, uint32_t *defer)
+{
+	lk();
+	*host_mem = g_last.host_mem;
+	*long_only = g_last.long_only;
+	*defer = g_last.defer != NULL;
+	ul();
+}
 unsigned long fakehip_inplace_frames(void) { lk(); unsigned long v = g_inplace; ul(); return v; }
 static void mem_add(const void *p, size_t n, int registered)
 {

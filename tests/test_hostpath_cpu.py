@@ -205,6 +205,31 @@ def test_async_one_completion_stamp_per_batch(fake, direct):
         assert lib.fakehip_stamps() - s0 == st["batches"], kind
 
 
+@pytest.mark.parametrize("kind,direct,want", [
+    ("tcp1514", True, (1, 1, 0)),    # long frames in host memory: the big-frame kernel alone
+    ("tcp1514", False, (0, 1, 0)),   # long frames copied to the device: the general kernel alone
+    ("imix", True, (1, 0, 1)),       # short frames present: the span kernel samples and defers
+    ("tcp64", True, (1, 0, 1)),
+])
+def test_async_launch_plan(fake, kind, direct, want):
+    """What the host tells the kernels about a batch (ixgrx_launch picks the
+    kernels from it): host memory, every frame >= IXG_LONG_ONLY_LEN, and
+    whether the deferral machinery is in use. Records as the oracle's."""
+    lib = fake.lib
+    rng = np.random.default_rng(0x5A)
+    tr, arena, ptrs = _mbufs(kind, 2000, seed=0x5A0)
+    eng = fake()
+    try:
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, "batch_frames": 512, "direct": direct})
+        m, r = _loop(eng, ptrs, rng)
+        hm, lo, df = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        lib.fakehip_last_plan(ctypes.byref(hm), ctypes.byref(lo), ctypes.byref(df))
+    finally:
+        eng.close()
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
+    assert (hm.value, lo.value, df.value) == want
+
+
 def test_async_aggregates_iterations(fake):
     """64-frame submissions are aggregated: 100 iterations of 64 frames with
     batch_frames 1600 make 4 launches, not 100."""
