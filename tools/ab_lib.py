@@ -7,6 +7,7 @@ change is judged only against a reference timed in the same process.
 usage: ab_lib.py --workload c4 --libs ix_amd/libixgrx.so,tools/ablib/base.so [--general]
 """
 import argparse
+import re
 import json
 import os
 import sys
@@ -34,7 +35,7 @@ def main():
     wl = bench.Workload(args.workload, seed=0x1B0002, dev=dev)
     engs = {}
     splits = args.splits.split(",") if args.splits else ["general" if args.general else "auto"]
-    for path in args.libs.split(","):
+    for path in re.split("[,+]", args.libs):
         for sp in splits:
             name = os.path.basename(path) + ("" if len(splits) == 1 else ":" + sp)
             engs[name] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags),
