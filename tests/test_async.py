@@ -284,13 +284,15 @@ def _filters_for(tr, pick):
     return f
 
 
-def test_set_fdir_with_batches_in_flight():
+@pytest.mark.parametrize("kind", ["tcp64", "tcp1514"])
+def test_set_fdir_with_batches_in_flight(kind):
     """ixg_rx_set_fdir from IX's connect path while the run loop has batches
     submitted and not yet polled: frames submitted before the call
     get the filters in force when they were submitted, frames after it the
-    new ones; every record against the oracle with the matching table."""
+    new ones; every record against the oracle with the matching table.
+    (1514-B frames: the host-memory big-frame kernel's flow-director match.)"""
     rng = np.random.default_rng(0x1F0)
-    tr, arena, ptrs = _mbufs("tcp64", 30000, seed=0x1F01)
+    tr, arena, ptrs = _mbufs(kind, 30000 if kind == "tcp64" else 12000, seed=0x1F01)
     offs = tr.offsets().astype(np.int64)
     tcp = np.nonzero(tr.blob[offs + 23] == 6)[0]
     f_old, f_new = _filters_for(tr, tcp[0::5]), _filters_for(tr, tcp[1::5])
