@@ -201,24 +201,29 @@ def test_gpu_async_reflect_golden(golden, which, direct):
 
 
 @pytest.mark.gpu
-def test_gpu_async_reflect_fuzz_vs_oracle():
+@pytest.mark.parametrize("long_only", [False, True])
+def test_gpu_async_reflect_fuzz_vs_oracle(long_only):
     """40K mixed frames (echo requests of every size up to 2 KiB, bad-checksum
     requests, TCP) through submit/poll with IXG_ASYNC_ICMP_REFLECT; a third
     of the mbufs come from an unregistered arena (left to the host's
-    icmp_reflect). Mbuf contents and records against the oracle."""
-    rng = np.random.default_rng(0x1C5)
-    n = 40000
+    icmp_reflect). Mbuf contents and records against the oracle. long_only:
+    20K frames of at least 256 B (the batches take the host-memory
+    big-frame kernel, then the reflect)."""
+    rng = np.random.default_rng(0x1C5 + long_only)
+    n = 20000 if long_only else 40000
+    lo = 256 - 42 if long_only else 0
     frames = []
     for i in range(n):
         u = rng.random()
         if u < 0.5:
-            frames.append(traces.icmp_echo(rng, int(rng.integers(0, 2048 - 42 + 1))))
+            frames.append(traces.icmp_echo(rng, int(rng.integers(lo, 2048 - 42 + 1))))
         elif u < 0.7:
-            f = bytearray(traces.icmp_echo(rng, int(rng.integers(0, 100))))
+            f = bytearray(traces.icmp_echo(rng, int(rng.integers(lo, lo + 100))))
             f[int(rng.integers(34, len(f)))] ^= 0x20
             frames.append(bytes(f))
         else:
-            frames.append(bytes(traces.build_ipv4(rng, 1, int(rng.choice([60, 590, 1514])), 6)[0]))
+            sizes = [590, 1514] if long_only else [60, 590, 1514]
+            frames.append(bytes(traces.build_ipv4(rng, 1, int(rng.choice(sizes)), 6)[0]))
     tr = traces.pack(frames)
     arena, ptrs = ixgrx.make_mbufs(tr)
     tr2 = traces.pack(frames)
