@@ -412,6 +412,18 @@ struct ixg_tcp_ext {
 int ixg_tcp_ext_batch_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec,
 			  uint32_t n, struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream);
 
+/* RX and the tcp_input head in one pass: d_out as ixg_rx_batch_dev, d_ext
+ * (and, with IXG_TCPX_INPLACE, the frames) as ixg_tcp_ext_batch_dev over
+ * those records. For a coalesced fixed-stride batch (stride <= 64 B, a
+ * 16-byte aligned base: 64-byte frames) the RX kernel writes each
+ * ixg_tcp_ext from the header bytes it has just parsed, with no second read
+ * of the frames or the records; other layouts run the two passes on
+ * `stream`. Replaces the pair ixg_rx_batch_dev + ixg_tcp_ext_batch_dev
+ * (dp/net/ip.c:120-141 through dp/net/tcp_in.c:230-241 per frame).
+ * Asynchronous on `stream`. 0 or -errno. */
+int ixg_rx_tcpx_batch_dev(void *ctx, const struct ixg_rx_frames *frames, uint32_t n, struct ixg_rx_rec *d_out,
+			  struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream);
+
 /* ---- ICMP echo reflect ---------------------------------------------------- */
 
 /* For every frame whose record is IXG_V_ICMP_ECHO, rewrite the frame in place

@@ -57,6 +57,8 @@ struct ixg_abatch {
 	uint32_t nic;
 	uint32_t *h_ic_idx;
 	uint64_t *h_ic_addr;
+	int dead;            /* its reflect ran but the batch could not be completed
+	                        (ixg_stage_launch -EPIPE): never launched again */
 };
 
 struct ixg_async {
@@ -202,6 +204,8 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	struct ixg_abatch *b = &a->b[last];
 	if (b->state != AS_OPEN)
 		return 0;
+	if (b->dead)
+		return -EIO;
 	HIPCHK(hipSetDevice(c->device));
 	struct ixg_stage st;
 	if (b->nabs)
@@ -219,6 +223,10 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	a->st.launch_ns += dt;
 	if (dt > a->st.launch_max_ns)
 		a->st.launch_max_ns = dt;
+	if (rc == -EPIPE) {
+		b->dead = 1;
+		return -EIO;
+	}
 	if (rc)
 		return rc;
 	b->state = AS_INFLIGHT;
@@ -248,6 +256,7 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
 	b->n = b->taken = 0;
 	b->nabs = b->nic = 0;
 	b->span = b->hi = b->link = 0;
+	b->dead = 0;
 	a->tail = (a->tail + 1) % a->cfg.depth;
 	a->count++;
 	return b;
@@ -414,7 +423,12 @@ int ixg_async_quiesce(struct ixg_ctx *c)
 #endif
 #define IXG_WAIT_QUERY_NS 1000000ull
 #define IXG_WAIT_RUNTIME_NS 200000000ull
-static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, int *napped)
+/* the caller's timer slack, saved when the naps set the wait's own */
+struct slack_save {
+	int changed;       /* PR_SET_TIMERSLACK was called: restore `saved` */
+	unsigned long saved;
+};
+static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, struct slack_save *sv)
 {
 	int queried = 0;
 	for (uint32_t k = 0;; k++) {
@@ -437,11 +451,16 @@ static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, int *
 		}
 		if (dt > IXG_WAIT_RUNTIME_NS)
 			return 1;
-		if (!*napped && IXG_WAIT_SLACK_NS > 0) {
-			*napped = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
-			prctl(PR_SET_TIMERSLACK, (unsigned long)IXG_WAIT_SLACK_NS, 0, 0, 0);
+		if (!sv->changed && IXG_WAIT_SLACK_NS > 0) {
+			const int cur = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+			/* a saved 0 could not be restored (PR_SET_TIMERSLACK 0 means
+			 * "the default"), and a slack already at the wait's needs no change */
+			if (cur > 0 && (unsigned long)cur != (unsigned long)IXG_WAIT_SLACK_NS &&
+			    prctl(PR_SET_TIMERSLACK, (unsigned long)IXG_WAIT_SLACK_NS, 0, 0, 0) == 0) {
+				sv->saved = (unsigned long)cur;
+				sv->changed = 1;
+			}
 		}
-		*napped |= 1 << 30;
 		const struct timespec nap = {0, IXG_WAIT_NAP_NS};
 		nanosleep(&nap, NULL);
 	}
@@ -449,10 +468,10 @@ static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, int *
 
 static int wait_done(struct ixg_ctx *c, struct ixg_abatch *b)
 {
-	int napped = 0; /* the caller's timer slack (+ 1 << 30) once naps began */
-	const int rc = wait_word(c, b, now_ns(), &napped);
-	if (napped && IXG_WAIT_SLACK_NS > 0)
-		prctl(PR_SET_TIMERSLACK, (unsigned long)(napped & ~(1 << 30)), 0, 0, 0);
+	struct slack_save sv = {0, 0};
+	const int rc = wait_word(c, b, now_ns(), &sv);
+	if (sv.changed)
+		prctl(PR_SET_TIMERSLACK, sv.saved, 0, 0, 0);
 	if (rc <= 0)
 		return rc;
 	HIPCHK(hipSetDevice(c->device));

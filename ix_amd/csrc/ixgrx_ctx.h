@@ -156,6 +156,11 @@ struct ixg_icmp_items {
 IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t lflags, hipStream_t s);
+/* ixg_launch_ds with the tcp_input head (ext != NULL: ixg_rx_tcpx_batch_dev) */
+IXG_INTERNAL int ixg_launch_x(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
+			      const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
+			      struct ixg_demux_rec *dmx, struct ixg_tcp_ext *ext, uint32_t xflags, uint32_t lflags,
+			      hipStream_t s);
 IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
 /* the per-chunk defer flags for batches of up to nchunks chunks (grown, never
  * shrunk; growing frees the old buffer, which waits for the device) */
@@ -232,7 +237,11 @@ IXG_INTERNAL void ixg_stage_finish_abs(uint8_t *buf, size_t span, size_t hi, con
  * reflect over `ic`'s candidates (if any), the D2H copy of the records into
  * h_rec; direct: the kernels read the pinned image and write h_rec
  * themselves (no copies). done_flag != NULL: then the completion stamp,
- * *done_flag = done_val (coherent pinned host memory), after all of it */
+ * *done_flag = done_val (coherent pinned host memory), after all of it.
+ * Returns -EIO when nothing that changes an mbuf was enqueued (the batch may
+ * be launched again). Once the reflect is enqueued a later failure completes
+ * the batch synchronously (stream wait, records, the word stored from the
+ * host); if even that fails, -EPIPE: the batch must not be launched again. */
 IXG_INTERNAL int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_stage *st, uint8_t *h_buf,
 		     uint8_t *d_buf, uint32_t n, struct ixg_rx_rec *d_rec, struct ixg_rx_rec *h_rec, int direct,
 		     const struct ixg_icmp_items *ic, uint32_t *done_flag, uint32_t done_val, hipStream_t s);

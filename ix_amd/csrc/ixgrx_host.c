@@ -264,6 +264,13 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t overlap, hipStream_t s)
 {
+	return ixg_launch_x(c, ds, base, off, len, stride, n, out, csum, dmx, NULL, 0, overlap, s);
+}
+
+int ixg_launch_x(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
+		 const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
+		 struct ixg_demux_rec *dmx, struct ixg_tcp_ext *ext, uint32_t xflags, uint32_t overlap, hipStream_t s)
+{
 	struct ixg_kparams p;
 	memset(&p, 0, sizeof(p));
 	p.base = base;
@@ -310,7 +317,28 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		p.epoch = ds->epoch;
 		p.force_mode = c->force_mode;
 	}
-	return ixgrx_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
+	if (!ext)
+		return ixgrx_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
+	/* the tcp_input head: fused into the coalesced fixed-shape kernel, else
+	 * the separate pass over the records behind the launch */
+	p.ext = ext;
+	p.xflags = xflags;
+	if (ixgrx_tcpx_fusable(&p))
+		return ixgrx_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
+	p.ext = NULL;
+	p.xflags = 0;
+	if (ixgrx_launch(&p, c->ncu, s) != 0)
+		return -EIO;
+	struct ixg_xparams xp;
+	memset(&xp, 0, sizeof(xp));
+	xp.base = (uint8_t *)(uintptr_t)base;
+	xp.off = off;
+	xp.rec = out;
+	xp.ext = ext;
+	xp.stride = stride;
+	xp.n = n;
+	xp.flags = xflags;
+	return ixgrx_tcpx_launch(&xp, s) == 0 ? 0 : -EIO;
 }
 
 /* the table: header {mask, fg, 0, 0} + slots (ixgrx_internal.h); the
@@ -681,7 +709,10 @@ void ixg_stage_finish(uint8_t *buf, size_t span, size_t hi, const uint64_t *off,
 	int uniform = off[0] == 0;
 	uint32_t lmin = 0xffffu, lmax = 0;
 	for (uint32_t k = 0; k < n; k++) {
-		uniform = uniform && off[k] == (uint64_t)k * s && len[k] <= s + 64u;
+		/* s == 0 (every offset 0): only a run of frames that stage nothing
+		 * (<= 12 bytes) is uniform; a longer frame staged its bytes at 0 and
+		 * would be wiped by the zeroed slots below */
+		uniform = uniform && off[k] == (uint64_t)k * s && len[k] <= s + 64u && (s || len[k] <= 12u);
 		lmin = len[k] < lmin ? len[k] : lmin;
 		lmax = len[k] > lmax ? len[k] : lmax;
 	}
@@ -833,10 +864,26 @@ int ixg_stage_launch(struct ixg_ctx *c, struct ixg_dstate *ds, const struct ixg_
 		if (ixgrx_icmp_launch(&p, s) != 0)
 			return -EIO;
 	}
-	if (!direct)
-		HIPCHK(hipMemcpyAsync(h_rec, d_rec, (size_t)n * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s));
-	if (done_flag && ixgrx_stamp(done_flag, done_val, s) != 0)
-		return -EIO;
+	int fail = 0;
+	if (!direct &&
+	    hipMemcpyAsync(h_rec, d_rec, (size_t)n * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost, s) != hipSuccess)
+		fail = 1;
+	if (!fail && done_flag && ixgrx_stamp(done_flag, done_val, s) != 0)
+		fail = 1;
+	if (!fail)
+		return 0;
+	if (!(ic && ic->n))
+		return -EIO; /* nothing enqueued has changed an mbuf: the caller may launch the batch again */
+	/* the reflect is enqueued: the mbufs become replies, so the batch cannot
+	 * be launched again (the parse would read the replies and the reflect
+	 * would swap them back). Complete it here: wait for the
+	 * stream, take the records, store the completion word from the host. */
+	if (hipStreamSynchronize(s) != hipSuccess)
+		return -EPIPE; /* the device failed under the batch: not retryable */
+	if (!direct && hipMemcpy(h_rec, d_rec, (size_t)n * sizeof(struct ixg_rx_rec), hipMemcpyDeviceToHost) != hipSuccess)
+		return -EPIPE;
+	if (done_flag)
+		__atomic_store_n(done_flag, done_val, __ATOMIC_RELEASE);
 	return 0;
 }
 
@@ -1100,6 +1147,23 @@ int ixg_rx_demux_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t 
 }
 
 /* ---- the rest of the tcp_input head (tcp_in.c:230-241) ---------------------- */
+
+int ixg_rx_tcpx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
+			  struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || (n && (!fr->base || !fr->len || !d_out || !d_ext)) || (flags & ~IXG_TCPX_INPLACE))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)fr->base & 3) || (!fr->off && (fr->stride & 3)) || ((uintptr_t)d_out & 15) ||
+	    ((uintptr_t)fr->len & 1) || ((uintptr_t)fr->off & 7) || ((uintptr_t)d_ext & 15))
+		return -EINVAL;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -EIO;
+	return ixg_launch_x(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, NULL,
+			    d_ext, flags, 0, (hipStream_t)stream);
+}
 
 int ixg_tcp_ext_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec, uint32_t n,
 			  struct ixg_tcp_ext *d_ext, uint32_t flags, void *stream)

@@ -133,6 +133,7 @@ DEV void mark_reply(const ixg_iparams& p, uint64_t r) {
 // the pages that hold lo and hi - 1 (so no access can fault); a piece only
 // partly inside [lo, hi) is stored byte by byte, only its bytes inside.
 constexpr uint32_t kSpanMax = 8192;
+constexpr uint32_t kMinEcho = 14u + 20u + 8u;  // the shortest frame icmp_input reflects
 
 template <bool OFFS>
 DEV bool flood_wave(const ixg_iparams& p, uint64_t i, int lane, bool valid, bool echo, uint32_t meta,
@@ -151,6 +152,12 @@ DEV bool flood_wave(const ixg_iparams& p, uint64_t i, int lane, bool valid, bool
   if (__builtin_amdgcn_ballot_w64(valid && (a < lo || re > kSpanMax - 16u)) != 0u) return false;
   const uint32_t pe = (uint32_t)__shfl_up((int)(uint32_t)re, 1, 64);
   if (__builtin_amdgcn_ballot_w64(valid && lane > 0 && (uint32_t)ra < pe) != 0u) return false;
+  // The span is stored back whole, gaps included. With u64 offsets another
+  // wave's frames may lie in this wave's gaps (a permuted offset array), and
+  // that wave rewrites them at the same time: take the span path
+  // only when no gap can hold an echo request (>= kMinEcho bytes: Ethernet,
+  // IPv4 and ICMP headers). Strided frames of other waves lie outside the span.
+  if (OFFS && __builtin_amdgcn_ballot_w64(valid && lane > 0 && (uint32_t)ra - pe >= kMinEcho) != 0u) return false;
   const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)re, nv - 1, 64);  // relative, the largest (ordered)
   const uintptr_t lo16 = lo & ~(uintptr_t)15;
   const uint32_t sh0 = (uint32_t)(lo - lo16);  // span start within the first piece

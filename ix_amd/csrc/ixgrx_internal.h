@@ -73,6 +73,11 @@ struct ixg_kparams {
 	uint32_t long_only;    /* every frame is at least 256 bytes (the host's
 	                          IXG_LF_LONG): with host_mem, the host-memory
 	                          big-frame kernel takes the batch */
+	/* the fused tcp_input head (ixg_rx_tcpx_batch_dev): ext != NULL turns
+	 * it on, in the kernels ixgrx_tcpx_fusable accepts */
+	struct ixg_tcp_ext *ext;
+	uint32_t xflags;       /* IXG_TCPX_* */
+	uint32_t rsvd;
 };
 
 /* the flow-director table's hash (host and device agree on it) */
@@ -139,6 +144,10 @@ int ixgrx_launch(const void *params, uint32_t ncu, void *stream);
  * everything enqueued before it on the stream */
 int ixgrx_stamp(uint32_t *flag, uint32_t v, void *stream);
 uint32_t ixgrx_kparams_size(void);
+/* 1 when ixgrx_launch writes p->ext itself (the coalesced fixed-shape
+ * kernel's layout in the default split, no fused demux); else the caller
+ * runs the separate tcp_input-head pass after the launch */
+int ixgrx_tcpx_fusable(const void *params);
 uint32_t ixgrx_block(void);
 
 #ifdef __cplusplus

@@ -31,6 +31,7 @@
 
 #include "../../include/ixgrx.h"
 #include "ixgrx_internal.h"
+#include "ixgrx_tcpx.h"
 #include "ixgrx_walk.h"
 
 #define DEV __device__ __forceinline__
@@ -1691,7 +1692,39 @@ DEV void dmx_finish(const KParams& p, const PendDmx& q, int lane, lds_u32* buf, 
 // tail past byte 96 (coalesced batches have strides <= 64 B, so such tails
 // only come from frames reaching into the following slots: rare). The IPv6
 // tables, when in use, are read from global memory (rare path: no LDS).
-template <bool DMX>
+// The fused tcp_input head (ixg_rx_tcpx_batch_dev; dp/net/tcp_in.c:230-241):
+// frame i's ixg_tcp_ext from its record and the five header dwords from 2
+// bytes before the TCP header, stored non-temporal (zero for a record that is
+// not IXG_V_TCP / IXG_V_TCP6), and with IXG_TCPX_INPLACE the in-place
+// conversion. ext_fixed: a fixed-shape frame (IPv4 ihl 5: the dwords are the
+// prefix's d[8..12], already in registers), stored through the chunk's
+// buffer resource (lanes past the batch drop). ext_reload: any frame, the
+// header loaded again (the coalesced kernel's rare non-fixed-shape chunks).
+DEV void ext_fixed(const KParams& p, uint32_t c, uint32_t rem, int lane, bool valid, const Rec& r,
+                   const uint32_t (&d)[kPrefixDw]) {
+  const bool tcp = ((r.w0 >> 16) & 0xffu) == IXG_V_TCP;
+  ixgx_ext e{0u, 0u, 0u, 0u};
+  if (tcp) e = ixgx_make(d[8], d[9], d[10], d[11], d[12], r.w1, r.w3);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{e.x, e.y, e.z, e.w}, rsrc(p.ext + (uint64_t)c * 64u, 16u * rem),
+                                         16 * lane, 0, kAuxNT);
+  if (tcp && valid && (p.xflags & IXG_TCPX_INPLACE))
+    ixgx_inplace(reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(p.base) + (uint64_t)(c * 64u + (uint32_t)lane) * p.stride + 32u),
+                 d[8], d[11], d[12], e);
+}
+DEV void ext_reload(const KParams& p, uint32_t i, uint64_t off, const Rec& r, const uint32_t (&d)[kPrefixDw]) {
+  const uint32_t v = (r.w0 >> 16) & 0xffu;
+  ixgx_ext e{0u, 0u, 0u, 0u};
+  if (v == IXG_V_TCP || v == IXG_V_TCP6) {
+    const uint32_t l4 = v == IXG_V_TCP6 ? 54u : 14u + 4u * (byte_at(d, 14) & 15u);
+    uint32_t* t = reinterpret_cast<uint32_t*>(const_cast<uint8_t*>(p.base) + off + l4 - 2u);
+    const uint32_t D0 = t[0], D1 = t[1], D2 = t[2], D3 = t[3], D4 = t[4];
+    e = ixgx_make(D0, D1, D2, D3, D4, r.w1, r.w3);
+    if (p.xflags & IXG_TCPX_INPLACE) ixgx_inplace(t, D0, D3, D4, e);
+  }
+  __builtin_nontemporal_store(u32x4{e.x, e.y, e.z, e.w}, reinterpret_cast<u32x4*>(p.ext + i));
+}
+
+template <bool DMX, bool TCPX = false>
 DEV void slow_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t chunk, int lane) {
   GDesc g;
   gen_desc<false>(p, chunk, lane, g);
@@ -1711,10 +1744,13 @@ DEV void slow_chunk(const KParams& p, const uint64_t* __restrict__ T, uint32_t c
   const Rec r = make_record(p, d, L, s, res);
   store_record(p, i, r, s.ip_res, res);
   store_demux<DMX>(p, i, r, s.src, s.dst, s.ports);
+  if (TCPX) ext_reload(p, i, g.off, r, d);
 }
 
-template <bool DMX, bool DRAIN = true>
+// TCPX: the fused tcp_input head (p.ext; not with DMX)
+template <bool DMX, bool DRAIN = true, bool TCPX = false>
 DEV void fastc_loop(const KParams& p, uint64_t* __restrict__ T, lds_u32* buf) {
+  static_assert(!(DMX && TCPX), "one fused pass at a time");
   const int lane = threadIdx.x & 63;
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t nchunks = (p.n + 63u) >> 6;
@@ -1824,6 +1860,18 @@ DEV void fastc_loop(const KParams& p, uint64_t* __restrict__ T, lds_u32* buf) {
         ports = s.ports;
       }
       dmx_issue(p, all_fast && valid, c, r, src, dst, ports, lane, pend);
+    } else if (TCPX) {
+      if (lean) {
+        const Rec r = lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * rem));
+        ext_fixed(p, c, rem, lane, valid, r, d);
+      } else if (all_fast) {
+        LaneState s;
+        lane_parse<kShapeFixed, kFastDw>(p, Tab64{T}, d, Lc, s);
+        const uint32_t r4 = l4_residual(s);
+        const Rec r = make_record<true>(p, d, Lc, s, r4);
+        if (valid) store_record<true>(p, i, r, s.ip_res, r4);
+        ext_fixed(p, c, rem, lane, valid, r, d);
+      }
     } else if (lean) {
       lean_tcp(p, T, i, lane, d, ipl, rsrc(p.out + (uint64_t)c * 64u, 16u * rem));
     } else if (all_fast) {
@@ -1847,7 +1895,7 @@ DEV void fastc_loop(const KParams& p, uint64_t* __restrict__ T, lds_u32* buf) {
   if (DRAIN) {
     // the wave's own deferred chunks (its first 64: a wave has ~8; the rest,
     // if any, were flagged for the general kernels above)
-    for (uint64_t m = dmask; m; m &= m - 1) slow_chunk<DMX>(p, T, chunk_of((uint32_t)__builtin_ctzll(m)), lane);
+    for (uint64_t m = dmask; m; m &= m - 1) slow_chunk<DMX, TCPX>(p, T, chunk_of((uint32_t)__builtin_ctzll(m)), lane);
   }
 }
 
@@ -1864,6 +1912,14 @@ ixg_rx_fastc_dmx_s(KParams p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t buf[kWaves][1024];
   fastc_loop<true>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
+}
+
+// with the fused tcp_input head (p.ext set: ixg_rx_tcpx_batch_dev)
+extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+ixg_rx_fastc_tcpx_s(KParams p) {
+  __shared__ uint64_t T[12 * 256];
+  __shared__ uint32_t buf[kWaves][1024];
+  fastc_loop<false, true, true>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
 }
 
 // ---- general kernel --------------------------------------------------------
@@ -2355,6 +2411,7 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
   const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&
                       (reinterpret_cast<uintptr_t>(p.base) & 15u) == 0u;
   const size_t sh6 = p.tab6 ? IXG_TAB6_WORDS * sizeof(uint32_t) : 0u;
+  if (p.ext && !ixgrx_tcpx_fusable(params)) return (int)hipErrorInvalidValue;  // (the host checks first)
   // offset and wide-stride batches in the default split: the span-staged
   // short kernel runs first and samples the mode itself (no sampler, no
   // fixed-shape kernel dispatch); forced splits and the fused demux keep the
@@ -2367,7 +2424,7 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
       // coalesced fixed stride: always fixed-shape first (no sampler),
       // unless a test forces another split
       if (forced) hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
-      if (!forced || p.force_mode == IXG_MODE_FAST) kf = p.dmx ? ixg_rx_fastc_dmx_s : ixg_rx_fastc_s;
+      if (!forced || p.force_mode == IXG_MODE_FAST) kf = p.dmx ? ixg_rx_fastc_dmx_s : p.ext ? ixg_rx_fastc_tcpx_s : ixg_rx_fastc_s;
     } else {
       hipLaunchKernelGGL(ixg_rx_sample, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
       kf = k_fast[lay];
@@ -2380,7 +2437,7 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
     // -> 0.3011 ms; profiles/r04/grid/); at least one block per 64 chunks
     // per wave, so every wave can finish its own deferred chunks
     // (fastc_loop's DRAIN)
-    const bool fc = kf == ixg_rx_fastc_s || kf == ixg_rx_fastc_dmx_s;
+    const bool fc = kf == ixg_rx_fastc_s || kf == ixg_rx_fastc_dmx_s || kf == ixg_rx_fastc_tcpx_s;
     const uint32_t gcu = fc ? 16u * ncu : ncu;
     if (kf) {
       uint64_t gb = grid_for(kf, wave_blocks, gcu);
@@ -2408,6 +2465,16 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, p.host_mem ? wave_blocks : group_blocks, ncu, sh6)), dim3(kBlock), sh6,
                      (hipStream_t)stream, p);
   return (int)hipGetLastError();
+}
+
+// the fused tcp_input head runs in the coalesced fixed-shape kernel alone
+// (ixg_rx_fastc_tcpx_s, which finishes every chunk of its batch itself): a
+// coalesced fixed-stride layout in the default split, no fused demux
+extern "C" int ixgrx_tcpx_fusable(const void* params) {
+  const KParams& p = *static_cast<const KParams*>(params);
+  const bool coal = !p.off && p.stride <= 64u && (p.stride & 3u) == 0u &&
+                    (reinterpret_cast<uintptr_t>(p.base) & 15u) == 0u;
+  return coal && p.defer && p.force_mode == IXG_MODE_AUTO && !p.dmx && !p.host_mem ? 1 : 0;
 }
 
 extern "C" uint32_t ixgrx_kparams_size(void) { return (uint32_t)sizeof(KParams); }

@@ -26,9 +26,6 @@ constexpr int kBlock = 256;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 u32x4_a4 __attribute__((aligned(4)));
 
-DEV uint32_t bswap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
-DEV uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
-
 // 20 header bytes from the dword boundary 2 bytes before the TCP header
 // (frame starts are 4-aligned and the header sits at 14 + 4*ihl or 54)
 struct Hdr {
@@ -58,24 +55,9 @@ DEV void tcpx(const ixg_xparams& p) {
     const uint32_t l4 = v6 ? 54u : 14u + 4u * ((w12 >> 16) & 15u);
     if (l4 != 34u) h = load_hdr(f + l4);  // IP options / IPv6: rare
     const uint32_t D0 = h.d.x, D1 = h.d.y, D2 = h.d.z, D3 = h.d.w, D4 = h.e;
-    const uint32_t src = bswap16(D0 >> 16);                   // tcp_in.c:230
-    const uint32_t dst = bswap16(D1 & 0xffffu);               // :231
-    const uint32_t seq = bswap32((D1 >> 16) | (D2 << 16));    // :236
-    const uint32_t ack = bswap32((D2 >> 16) | (D3 << 16));    // :237
-    const uint32_t wnd = bswap16(D4 & 0xffffu);               // :238
-    // :240-241: p->tot_len after the doff strip (the record's l4_len), +1
-    // for FIN or SYN (TCP_FIN | TCP_SYN = 0x03), kept as u16
-    const uint32_t tcplen = ((r.y >> 16) + (((r.w >> 16) & 3u) ? 1u : 0u)) & 0xffffu;
-    x = u32x4{seq, ack, wnd | (tcplen << 16), src | (dst << 16)};
-    if (p.flags & IXG_TCPX_INPLACE) {
-      // tcp_in.c:230-238 writes the same fields back in host order
-      uint32_t* t = reinterpret_cast<uint32_t*>(f + l4 - 2);
-      t[0] = (D0 & 0xffffu) | (src << 16);
-      t[1] = dst | (seq << 16);
-      t[2] = (seq >> 16) | (ack << 16);
-      t[3] = (ack >> 16) | (D3 & 0xffff0000u);
-      t[4] = wnd | (D4 & 0xffff0000u);
-    }
+    const ixgx_ext e = ixgx_make(D0, D1, D2, D3, D4, r.y, r.w);
+    x = u32x4{e.x, e.y, e.z, e.w};
+    if (p.flags & IXG_TCPX_INPLACE) ixgx_inplace(reinterpret_cast<uint32_t*>(f + l4 - 2), D0, D3, D4, e);
   }
   __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p.ext) + i);
 }

@@ -21,7 +21,7 @@ TCPX_DTYPE = np.dtype([("seqno", "<u4"), ("ackno", "<u4"), ("wnd", "<u2"), ("tcp
                        ("src_port", "<u2"), ("dst_port", "<u2")])
 assert TCPX_DTYPE.itemsize == 16
 IXG_TCPX_INPLACE = 1 << 0
-EXPORTS = ("ixg_tcp_ext_batch_dev",)
+EXPORTS = ("ixg_tcp_ext_batch_dev", "ixg_rx_tcpx_batch_dev")
 
 
 def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
@@ -30,6 +30,8 @@ def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     lib.ixg_tcp_ext_batch_dev.argtypes = [vp, ctypes.POINTER(ixgrx.RxFrames), vp, u32, vp, u32, vp]
     lib.ixg_tcp_ext_batch_dev.restype = i32
+    lib.ixg_rx_tcpx_batch_dev.argtypes = [vp, ctypes.POINTER(ixgrx.RxFrames), u32, vp, vp, u32, vp]
+    lib.ixg_rx_tcpx_batch_dev.restype = i32
     lib._ixg_tcpx_bound = True
     return lib
 
@@ -42,3 +44,15 @@ def batch_dev(eng: ixgrx.RxEngine, base: int, off: int | None, stride: int, rec:
     fr = ixgrx.RxFrames(base, off or None, 0, stride, 0)
     ixgrx._check(lib.ixg_tcp_ext_batch_dev(eng._ctx, ctypes.byref(fr), rec, n, ext, flags, stream or None),
                  "ixg_tcp_ext_batch_dev", lib)
+
+
+def rx_batch_dev(eng: ixgrx.RxEngine, base: int, off: int | None, lens: int, stride: int, n: int, rec: int,
+                 ext: int, flags: int = 0, stream: int | None = None) -> None:
+    """ixg_rx_tcpx_batch_dev: RX records and the tcp_input head in one pass
+    (fused into the coalesced fixed-shape kernel for 64-byte strides; other
+    layouts run RX, then the separate pass). Device pointers (int);
+    asynchronous on `stream`."""
+    lib = _bind(eng._lib)
+    fr = ixgrx.RxFrames(base, off or None, lens, stride, 0)
+    ixgrx._check(lib.ixg_rx_tcpx_batch_dev(eng._ctx, ctypes.byref(fr), n, rec, ext, flags, stream or None),
+                 "ixg_rx_tcpx_batch_dev", lib)

@@ -67,6 +67,8 @@ static unsigned long g_launches;
 static int g_fail_launches;      /* the next this many RX launches fail */
 static unsigned long g_fdir_stale; /* RX launches that ran after their table changed */
 void fakehip_fail_launches(int k) { lk(); g_fail_launches = k; ul(); }
+static int g_fail_stamps;        /* the next this many completion stamps fail to launch */
+void fakehip_fail_stamps(int k) { lk(); g_fail_stamps = k; ul(); }
 unsigned long fakehip_fdir_stale(void) { lk(); unsigned long v = g_fdir_stale; ul(); return v; }
 
 /* FNV-1a over the flow-director table a launch reads (header + slots) */
@@ -481,6 +483,11 @@ int ixgrx_stamp(uint32_t *flag, uint32_t v, void *stream)
 	lk();
 	if (!reachable((uintptr_t)flag, (uintptr_t)(flag + 1)))
 		abort();
+	if (g_fail_stamps > 0) {
+		g_fail_stamps--;
+		ul();
+		return -1;
+	}
 	struct op *o = new_op(OP_STAMP);
 	o->dst = flag;
 	o->val = (int)v;
@@ -512,6 +519,11 @@ int ixgrx_icmp_launch(const void *p, void *s)
 	lk();
 	push((hipStream_t)s, o);
 	ul();
+	return 0;
+}
+int ixgrx_tcpx_fusable(const void *p)
+{
+	(void)p;
 	return 0;
 }
 int ixgrx_tcpx_launch(const void *p, void *s)

@@ -81,7 +81,10 @@ def test_tiny_frames(fake):
     """Frames of 0..13 bytes (nothing or one byte past the MACs staged), in
     a batch of one length (fixed-stride staging) and mixed."""
     rng = np.random.default_rng(3)
-    for lens in ([5] * 300, list(rng.integers(0, 14, 500)), [12] * 70, [13] * 65):
+    # ADVICE r05: runs where every frame but the last stages nothing (<= 12 B)
+    # have all offsets 0; they are not a fixed-stride run
+    for lens in ([5] * 300, list(rng.integers(0, 14, 500)), [12] * 70, [13] * 65, [10, 10, 60], [5] * 63 + [60],
+                 [12] * 64 + [64], [0, 60]):
         frames = [bytes(rng.integers(0, 256, int(L), dtype=np.uint8)) for L in lens]
         tr = traces.pack(frames)
         arena, ptrs = ixgrx.make_mbufs(tr)
@@ -625,3 +628,64 @@ def test_async_icmp_reflect_needs_registered_mbufs(fake):
         eng.close()
     assert np.array_equal(r.view(np.uint8).reshape(-1, 16), _expect(ptrs))
     assert np.array_equal(arena, before)
+
+
+@pytest.mark.parametrize("direct", [True, False])
+@pytest.mark.parametrize("inject", ["stamp", "launch"])
+def test_async_icmp_reflect_failures_reflect_once(fake, direct, inject):
+    """a launch that fails after the echo reflect was enqueued
+    (the completion stamp, here) must not leave the batch to be launched
+    again: the retry would parse the replies and reflect them back into
+    requests. Such a batch is completed on the spot; a batch whose RX launch
+    itself fails (nothing enqueued has touched an mbuf) is retried. Either
+    way every echo request comes back reflected exactly once, as the
+    reference's icmp_input leaves it (tests/golden/icmp.npz)."""
+    fake.lib.fakehip_fail_stamps.argtypes = [ctypes.c_int]
+    g = dict(np.load(os.path.join(ROOT, "tests", "golden", "icmp.npz")))
+    tr = traces.Trace(blob=g["blob"].copy(), off=g["off"], len=g["len"], stride=0)
+    arena, ptrs = ixgrx.make_mbufs(tr)
+    exp = _expect(ptrs)
+    refl = g["reflected"].astype(bool)
+    rng = np.random.default_rng(11)
+    eng = fake()
+    errors = 0
+    try:
+        eng.async_init(batch_frames=24, batch_bytes=1 << 20, max_wait_us=10000000, depth=3, direct=direct,
+                       icmp_reflect=True)
+        eng.register_memory(arena.ctypes.data, arena.nbytes)
+        eng.set_icmp_reply(bytes(g["mac"]), int(g["host_addr"]))
+        got_m, got_r = [], []
+        i = 0
+        while i < len(ptrs) or eng.pending():
+            if i < len(ptrs) and rng.integers(0, 3) == 0:
+                (fake.lib.fakehip_fail_stamps if inject == "stamp" else fake.lib.fakehip_fail_launches)(1)
+            acc = 0
+            if i < len(ptrs):
+                k = int(rng.integers(1, 17))
+                try:
+                    acc = eng.submit_mbufs(ptrs[i:i + k])
+                except RuntimeError:
+                    errors += 1
+                    continue
+                i += acc
+            try:
+                m, r = eng.poll(1000, wait=acc == 0)
+            except RuntimeError:
+                errors += 1
+                continue
+            got_m.append(m)
+            got_r.append(r)
+        fake.lib.fakehip_fail_stamps(0)
+        fake.lib.fakehip_fail_launches(0)
+    finally:
+        eng.close()
+    if inject == "launch":
+        assert errors > 0
+    m, r = np.concatenate(got_m), np.concatenate(got_r)
+    assert np.array_equal(m, ptrs)
+    want = exp.copy()
+    want[refl, 3] |= ixgrx.RF_REPLY
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), want)
+    base = arena.ctypes.data
+    for j, (p, o, L) in enumerate(zip(ptrs.astype(np.int64), g["off"].astype(np.int64), g["len"].astype(np.int64))):
+        assert np.array_equal(arena[p - base + 64:p - base + 64 + L], g["after"][o:o + L]), j

@@ -260,19 +260,30 @@ def test_gpu_async_reflect_fuzz_vs_oracle(long_only):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["packed", "unaligned", "stride", "gaps"])
+@pytest.mark.parametrize("layout", ["packed", "unaligned", "stride", "gaps", "interleaved"])
 def test_gpu_flood_span_path(layout):
     """Waves whose 64 items are all small echo requests in increasing,
     non-overlapping order take the span path (the wave's frames staged in LDS
     and stored back whole): every byte of the buffer, gaps and the bytes
     around each wave's span included, against the oracle; message lengths
-    8..128 bytes, a partial last wave, spans at every 16-byte phase."""
+    8..128 bytes, a partial last wave, spans at every 16-byte phase.
+    interleaved: packed small pings whose offset array deals
+    each run of 128 frames out to two waves, even frames to one and odd to
+    the other, so each wave's gaps hold the other wave's frames, which it
+    rewrites at the same time: no wave may store its gaps back."""
     rng = np.random.default_rng(0x1C6)
     key = traces.RSS_KEY
     mac, host = bytes([2, 4, 6, 8, 10, 12]), 0x0a000001
     n = 64 * 200 + 37
-    frames = [traces.icmp_echo(rng, int(rng.integers(0, 121))) for _ in range(n)]
-    if layout == "stride":
+    frames = [traces.icmp_echo(rng, int(rng.integers(0, 21 if layout == "interleaved" else 121))) for _ in range(n)]
+    if layout == "interleaved":
+        tr = traces.pack(frames)
+        perm = np.arange(n)
+        m = n - n % 128
+        perm[:m] = perm[:m].reshape(-1, 64, 2).transpose(0, 2, 1).reshape(-1)
+        frames = [frames[j] for j in perm]
+        tr = traces.Trace(blob=tr.blob, off=tr.off[perm].copy(), len=tr.len[perm].copy(), stride=0)
+    elif layout == "stride":
         tr = traces.pack(frames, stride=192)
     elif layout == "gaps":
         # random 0..40-byte gaps of random bytes between the frames

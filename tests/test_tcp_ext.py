@@ -202,3 +202,118 @@ def test_oracle_ext_vs_reference_fresh_fuzz():
         for i in tcp:
             s = int(tr.off[i]) + 14 + 4 * int(ihl[i])
             assert bytes(b[s:s + 16]) == bytes(hdr[i])
+
+
+# ---------------------------------------------------------------- fused RX + head (ixg_rx_tcpx_batch_dev)
+
+def _fused_run(eng, blob, off, lens, stride, flags=0):
+    """Upload a batch, run ixg_rx_tcpx_batch_dev, return (records, ext, frames after)."""
+    import torch
+    from ix_amd import ixgrx, tcpx
+    dev = torch.device("cuda", 0)
+    n = int(lens.shape[0])
+    b = torch.from_numpy(np.concatenate([np.ascontiguousarray(blob, dtype=np.uint8),
+                                         np.zeros(ixgrx.IXG_TAIL_PAD, np.uint8)])).to(dev)
+    o = None if off is None else torch.from_numpy(np.ascontiguousarray(off, dtype=np.uint64).view(np.int64)).to(dev)
+    ln = torch.from_numpy(np.ascontiguousarray(lens, dtype=np.uint16).view(np.int16)).to(dev)
+    rec = torch.full((max(n, 1), 16), 0x5A, dtype=torch.uint8, device=dev)
+    ext = torch.full((max(n, 1), 16), 0xA5, dtype=torch.uint8, device=dev)
+    tcpx.rx_batch_dev(eng, b.data_ptr(), None if o is None else o.data_ptr(), ln.data_ptr(), stride, n,
+                      rec.data_ptr(), ext.data_ptr(), flags, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return rec[:n].cpu().numpy(), ext[:n].cpu().numpy(), b.cpu().numpy()[:blob.size]
+
+
+def _golden_engine(g):
+    from ix_amd import ixgrx
+    eng = ixgrx.RxEngine(ixgrx.Config(bytes(g["key"]), int(g["nb_rx_fgs"]), int(g["dev_idx"]), int(g["flags"])))
+    if "fdir" in g:
+        eng.set_fdir(np.ascontiguousarray(g["fdir"]).view(ixgrx.FDIR_DTYPE).reshape(-1), int(g["fdir_cpu"]))
+    return eng
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stride", [60, 64])
+@pytest.mark.parametrize("flags", [0, INPLACE])
+def test_gpu_fused_golden_fixed_stride(golden, stride, flags):
+    """the golden frames of at most `stride` bytes (every
+    edge case of the fixture that fits a 64-byte slot: bad checksums, IP
+    options, short segments, drops) in one coalesced fixed-stride batch, so
+    the fused coalesced kernel takes them (its lean, fixed-shape and
+    general-parse chunks): records against the reference's, ext against its
+    tcp_input's LWIP_Context fields (`tcpx`), frames after against its
+    in-place conversion (`tcpx_hdr`)."""
+    sel = np.nonzero(golden["len"].astype(np.int64) <= stride)[0]
+    if sel.size == 0:
+        pytest.skip("no frame fits the stride")
+    # repeated so the batch spans many chunks and waves, with a ragged end
+    reps = max(1, 5000 // sel.size)
+    idx = np.tile(sel, reps)[:max(sel.size, min(5000, sel.size * reps) - 17)]
+    n = idx.size
+    blob = np.zeros(n * stride + 64, np.uint8)
+    offs = golden["off"].astype(np.int64)
+    lens = golden["len"].astype(np.int64)
+    for k, i in enumerate(idx):
+        blob[k * stride:k * stride + lens[i]] = golden["blob"][offs[i]:offs[i] + lens[i]]
+    eng = _golden_engine(golden)
+    try:
+        rec, ext, after = _fused_run(eng, blob, None, lens[idx].astype(np.uint16), stride, flags)
+    finally:
+        eng.close()
+    bad = np.nonzero((rec != golden["rec"][idx]).any(axis=1))[0]
+    assert bad.size == 0, f"{golden['name']}: {bad.size} records differ, first {bad[:6].tolist()}"
+    bad = np.nonzero((ext != golden["tcpx"][idx]).any(axis=1))[0]
+    assert bad.size == 0, f"{golden['name']}: {bad.size} ext differ, first {bad[:6].tolist()}: " \
+                          f"{ext[bad[0]].tolist()} vs {golden['tcpx'][idx[bad[0]]].tolist()}"
+    _, eb = oracle.tcp_ext_batch(blob, None, stride, golden["rec"][idx], flags)
+    assert (after == eb[:after.size]).all(), "frames after the fused kernel differ from the in-place conversion"
+    if flags:
+        l4, v = _l4(golden)
+        for k, i in enumerate(idx[:2000]):
+            if v[i] in (TCP, TCP6):
+                s = k * stride + int(l4[i])
+                assert bytes(after[s:s + 16]) == bytes(golden["tcpx_hdr"][i]), (golden["name"], k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,n,stride", [("tcp64", 300000, 60), ("tcp64", 70000, 64), ("tcp64opt", 30000, 64),
+                                           ("imix", 40000, 0), ("mixed", 20000, 0), ("tcp1514", 3000, 0)])
+@pytest.mark.parametrize("flags", [0, INPLACE])
+def test_gpu_fused_vs_oracle(kind, n, stride, flags):
+    """Synthetic traces, 1 % bad checksums: C2's shape (stride 60, the fused
+    kernel's lean path), stride 64, IP options in 64-byte slots (the fused
+    kernel's general-parse chunks), and the layouts the fused kernel does not
+    take (u64 offsets: RX, then the separate pass): records, ext and frames
+    bit-exact against the oracle."""
+    from ix_amd import ixgrx
+    tr = traces.make_trace(kind, n, seed=0x7E0 + n, bad_ip=0.01, bad_l4=0.01)
+    if stride and tr.stride != stride:
+        frames = [tr.frame(i) for i in range(tr.n)]
+        assert max(len(f) for f in frames) <= stride
+        tr = traces.pack(frames, stride=stride)
+    er, _ = oracle.rx_trace(tr, traces.RSS_KEY, threads=8)
+    eext, eb = oracle.tcp_ext_batch(tr.blob, tr.off, tr.stride, er, flags)
+    eng = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY))
+    try:
+        rec, ext, after = _fused_run(eng, tr.blob, None if tr.stride else tr.off, tr.len, tr.stride, flags)
+    finally:
+        eng.close()
+    assert (rec == er).all(), kind
+    bad = np.nonzero((ext != eext).any(axis=1))[0]
+    assert bad.size == 0, f"{kind}: {bad.size} ext differ, first {bad[:6].tolist()}"
+    assert (after == eb[:after.size]).all(), kind
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 257, 4097])
+def test_gpu_fused_ragged(n):
+    from ix_amd import ixgrx
+    tr = traces.make_trace("tcp64", n, seed=0x7F0 + n, bad_ip=0.05, bad_l4=0.05)
+    er, _ = oracle.rx_trace(tr, traces.RSS_KEY)
+    eext, _ = oracle.tcp_ext_batch(tr.blob, tr.off, tr.stride, er)
+    eng = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY))
+    try:
+        rec, ext, _ = _fused_run(eng, tr.blob, None, tr.len, tr.stride)
+    finally:
+        eng.close()
+    assert (rec == er).all() and (ext == eext).all()
