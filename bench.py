@@ -1130,6 +1130,13 @@ def summary(res: dict) -> dict:
         top = max((k for k in lp if k.startswith("threads") and k[7:].isdigit()), key=lambda k: int(k[7:]), default=None)
         if top:
             out["host_path"]["t%s_max_latency_us" % top[7:]] = lp[top].get("latency_us", {}).get("max")
+        # the worst batch of the zero-copy line, split where its time went
+        # (ixg_rx_async_stats: open / gpu / visible / returned; wait, outside)
+        zc = next((k for k in lp if k.endswith("_zero_copy")), None)
+        if zc and "worst_batch_us" in lp[zc]:
+            w = lp[zc]["worst_batch_us"]
+            out["host_path"]["zc_worst_us"] = {k: w[k] for k in ("total", "open", "gpu", "visible", "returned",
+                                                                  "outside") if k in w}
         out["host_path"]["parity"] = hp.get("parity")
     if "cpu_baseline" in res:
         out["cpu_baseline_mpps"] = res["cpu_baseline"]["value"]

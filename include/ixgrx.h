@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define IXGRX_ABI_VERSION 2
+#define IXGRX_ABI_VERSION 3
 
 /* Constants of the reference this ABI is bit-exact against. */
 #define IXG_ETH_MAX_NUM_FG 512u    /* inc/ix/ethfg.h:38 ETH_MAX_NUM_FG */
@@ -272,6 +272,19 @@ struct ixg_rx_async_stats {
 	uint64_t inplace_bytes;    /* in-place (zero-copy) frames of the launched batches, in
 	                              64-B requests */
 	uint64_t frames_launched;  /* frames of the launched batches */
+	/* The batch whose first frame waited longest from its gather to the poll
+	 * that returned its last frame (the worst frame latency of the window),
+	 * split where the time went: open = first frame gathered -> batch
+	 * launched; gpu = launched -> the completion stamp ran on the device (its
+	 * wall clock, calibrated to CLOCK_MONOTONIC at ixg_rx_async_init; 0 when
+	 * unknown); visible = stamp ran -> the library saw the completion word
+	 * (the thread was not polling, or was asleep in the wait); returned =
+	 * seen -> the last frame handed back by poll. open + gpu + visible +
+	 * returned = total. wait: time poll(wait) blocked on this batch; outside:
+	 * the longest interval between two calls into the library while the batch
+	 * was pending (the caller's own work, or the thread off its CPU). */
+	uint64_t worst_total_ns, worst_open_ns, worst_gpu_ns, worst_visible_ns, worst_returned_ns;
+	uint64_t worst_wait_ns, worst_outside_ns;
 };
 /* Copy the counters to *out (may be NULL) and, reset != 0, zero them. 0 or -errno. */
 int ixg_rx_async_stats(void *ctx, struct ixg_rx_async_stats *out, int reset);

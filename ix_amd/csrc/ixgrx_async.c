@@ -59,6 +59,9 @@ struct ixg_abatch {
 	uint64_t *h_ic_addr;
 	int dead;            /* its reflect ran but the batch could not be completed
 	                        (ixg_stage_launch -EPIPE): never launched again */
+	/* where its frames' time goes (ixg_rx_async_stats' worst batch): ns */
+	uint64_t t_launch, t_seen, t_gpu, wait_ns;
+	uint64_t gap_max;    /* TSC ticks: longest interval outside the library while pending */
 };
 
 struct ixg_async {
@@ -72,6 +75,10 @@ struct ixg_async {
 	                        frames: reported (and cleared) by the next
 	                        submit / poll / flush; the batch stays OPEN */
 	size_t bytes_cap;    /* gathered-bytes capacity of a batch */
+	uint64_t t_exit;     /* TSC: the last return from submit / poll (0: none yet) */
+	/* the device's wall clock -> CLOCK_MONOTONIC ns: ns = ticks * gclk_mul + gclk_off
+	 * (gclk_mul 0: unknown) */
+	double gclk_mul, gclk_off;
 	struct ixg_abatch b[IXG_ASYNC_MAX_DEPTH];
 };
 
@@ -129,8 +136,9 @@ static int batch_alloc(struct ixg_async *a, struct ixg_abatch *b)
 	const uint32_t nf = a->cfg.batch_frames;
 	const size_t bcap = IXG_STAGE_BYTES(a->bytes_cap, nf);
 	HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
-	HIPCHK(hipHostMalloc((void **)&b->h_done, sizeof(uint32_t), hipHostMallocCoherent));
-	*b->h_done = 0;
+	/* the completion word and the stamp's device clock (ixgrx_stamp) */
+	HIPCHK(hipHostMalloc((void **)&b->h_done, 4 * sizeof(uint32_t), hipHostMallocCoherent));
+	memset(b->h_done, 0, 4 * sizeof(uint32_t));
 	HIPCHK(hipMalloc((void **)&b->ds.d_present, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 	HIPCHK(hipMemset(b->ds.d_present, 0, IXG_PRESENT_WORDS * sizeof(uint32_t)));
 	const int rc = ixg_dstate_reserve(&b->ds, ((size_t)nf + 63u) / 64u);
@@ -153,6 +161,84 @@ static int batch_alloc(struct ixg_async *a, struct ixg_abatch *b)
 		return -ENOMEM;
 	memset(b->h_buf, 0, bcap);
 	return 0;
+}
+
+/* The device wall clock (the stamp's, wall_clock64) against CLOCK_MONOTONIC:
+ * a stamp on batch 0's stream between two host clock readings, three times,
+ * the tightest bracket kept. Its rate comes from the device attribute. On
+ * failure the split reports no device time (gclk_mul 0). */
+static void clock_calibrate(struct ixg_ctx *c, struct ixg_async *a)
+{
+	int khz = 0;
+	if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device) != hipSuccess || khz <= 0)
+		return;
+	struct ixg_abatch *b = &a->b[0];
+	uint64_t best = ~0ull;
+	double off = 0;
+	const double mul = 1e6 / (double)khz;
+	int ok = 1;
+	for (int k = 0; k < 3 && ok; k++) {
+		b->h_done[0] = 0;
+		const uint64_t t0 = now_ns();
+		ok = ixgrx_stamp(b->h_done, 0x7fffffffu, b->stream) == 0 && hipStreamSynchronize(b->stream) == hipSuccess;
+		const uint64_t t1 = now_ns();
+		const uint64_t g = (uint64_t)b->h_done[2] | ((uint64_t)b->h_done[3] << 32);
+		ok = ok && __atomic_load_n(b->h_done, __ATOMIC_ACQUIRE) == 0x7fffffffu && g != 0;
+		if (ok && t1 - t0 < best) {
+			best = t1 - t0;
+			off = (double)(t0 + (t1 - t0) / 2) - (double)g * mul;
+		}
+	}
+	memset(b->h_done, 0, 4 * sizeof(uint32_t)); /* (the batch's first launch stores 1) */
+	if (ok) {
+		a->gclk_mul = mul;
+		a->gclk_off = off;
+	}
+}
+
+/* time outside the library: on entry to submit / poll, the interval since the
+ * last return, charged to every pending batch */
+static void entry_gap(struct ixg_async *a)
+{
+	if (!a->t_exit || !a->count)
+		return;
+	const uint64_t g = tsc() - a->t_exit;
+	for (uint32_t k = 0, i = a->head; k < a->count; k++, i = (i + 1) % a->cfg.depth)
+		if (g > a->b[i].gap_max)
+			a->b[i].gap_max = g;
+}
+
+/* a batch's last frame was returned at t (ns): the window's worst batch so far? */
+static void batch_returned(struct ixg_async *a, const struct ixg_abatch *b, uint64_t t)
+{
+	const uint64_t tot = t - b->t_open;
+	if (tot <= a->st.worst_total_ns)
+		return;
+	a->st.worst_total_ns = tot;
+	a->st.worst_open_ns = b->t_launch - b->t_open;
+	uint64_t gpu = 0, vis = b->t_seen - b->t_launch;
+	if (b->t_gpu >= b->t_launch && b->t_gpu <= b->t_seen) {
+		gpu = b->t_gpu - b->t_launch;
+		vis = b->t_seen - b->t_gpu;
+	}
+	a->st.worst_gpu_ns = gpu;
+	a->st.worst_visible_ns = vis;
+	a->st.worst_returned_ns = t - b->t_seen;
+	a->st.worst_wait_ns = b->wait_ns;
+	a->st.worst_outside_ns = b->gap_max; /* (ticks: converted when read) */
+}
+
+/* the library saw batch b's completion word (its stamp's device clock: when
+ * the stamp ran, in CLOCK_MONOTONIC ns; 0 when unknown) */
+static void batch_seen(const struct ixg_async *a, struct ixg_abatch *b)
+{
+	b->t_seen = now_ns();
+	b->t_gpu = 0;
+	if (a->gclk_mul > 0) {
+		const uint64_t g = (uint64_t)b->h_done[2] | ((uint64_t)b->h_done[3] << 32);
+		const double t = (double)g * a->gclk_mul + a->gclk_off;
+		b->t_gpu = t > 0 ? (uint64_t)t : 0;
+	}
 }
 
 int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
@@ -191,6 +277,7 @@ int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
 			return rc;
 		}
 	}
+	clock_calibrate(c, a);
 	return 0;
 }
 
@@ -230,6 +317,7 @@ static int launch_open(struct ixg_ctx *c, struct ixg_async *a)
 	if (rc)
 		return rc;
 	b->state = AS_INFLIGHT;
+	b->t_launch = now_ns();
 	a->st.batches++;
 	a->st.image_bytes += st.h2d;
 	a->st.inplace_bytes += b->link;
@@ -257,6 +345,7 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
 	b->nabs = b->nic = 0;
 	b->span = b->hi = b->link = 0;
 	b->dead = 0;
+	b->wait_ns = b->gap_max = 0;
 	a->tail = (a->tail + 1) % a->cfg.depth;
 	a->count++;
 	return b;
@@ -313,6 +402,7 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 		a->err = 0;
 		return e;
 	}
+	entry_gap(a);
 	const uint64_t t = now_ns();
 	uint32_t done = 0;
 	a->st.submit_calls++;
@@ -361,6 +451,7 @@ int ixg_rx_submit_mbufs(void *vctx, void *const *mbufs, uint32_t n)
 	}
 	a->st.frames_submitted += done;
 	a->st.frames_refused += n - done;
+	a->t_exit = tsc();
 	return (int)done;
 }
 
@@ -494,8 +585,11 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 	if (!a)
 		return 0;
 	a->st.poll_calls++;
-	if (!a->count || !max)
+	entry_gap(a);
+	if (!a->count || !max) {
+		a->t_exit = tsc();
 		return 0;
+	}
 	/* an OPEN batch whose oldest frame has waited long enough goes now */
 	{
 		const struct ixg_abatch *o = &a->b[(a->tail + a->cfg.depth - 1) % a->cfg.depth];
@@ -513,12 +607,14 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 			if (__atomic_load_n(b->h_done, __ATOMIC_ACQUIRE) != b->seq) {
 				if (!wait || got)
 					break;
-				const uint64_t w0 = tsc();
+				const uint64_t w0 = tsc(), n0 = now_ns();
 				const int rc = wait_done(c, b);
 				a->st.wait_ns += tsc() - w0;
+				b->wait_ns += now_ns() - n0;
 				if (rc)
 					return rc;
 			}
+			batch_seen(a, b);
 			b->state = AS_DONE;
 		}
 		if (b->state != AS_DONE)
@@ -529,13 +625,15 @@ int ixg_rx_poll(void *vctx, void **mbufs, struct ixg_rx_rec *recs, uint32_t max,
 		b->taken += k;
 		got += k;
 		if (b->taken == b->n) {
+			batch_returned(a, b, now_ns());
 			b->state = AS_FREE;
 			a->head = (a->head + 1) % a->cfg.depth;
 			a->count--;
 		}
 	}
 	a->st.frames_returned += got;
-	a->st.poll_ns += tsc() - p0;
+	a->t_exit = tsc();
+	a->st.poll_ns += a->t_exit - p0;
 	return (int)got;
 }
 
@@ -558,6 +656,7 @@ int ixg_rx_async_stats(void *vctx, struct ixg_rx_async_stats *out, int reset)
 			out->poll_ns = (uint64_t)((double)(a->st.poll_ns - a->st.wait_ns) * r);
 			out->wait_ns = (uint64_t)((double)a->st.wait_ns * r);
 		out->launch_max_ns = (uint64_t)((double)a->st.launch_max_ns * r);
+			out->worst_outside_ns = (uint64_t)((double)a->st.worst_outside_ns * r);
 		}
 	}
 	if (reset && a)

@@ -141,7 +141,8 @@ IXG_HD static inline uint32_t ixg_demux_group(uint32_t fg_id, uint32_t fg_base, 
  * occupancy */
 int ixgrx_launch(const void *params, uint32_t ncu, void *stream);
 /* enqueue the completion stamp: *flag = v (coherent pinned host memory), after
- * everything enqueued before it on the stream */
+ * everything enqueued before it on the stream; flag[2..3] = the device's wall
+ * clock (wall_clock64) when it ran, stored before flag[0] (flag: 16 bytes) */
 int ixgrx_stamp(uint32_t *flag, uint32_t v, void *stream);
 uint32_t ixgrx_kparams_size(void);
 /* 1 when ixgrx_launch writes p->ext itself (the coalesced fixed-shape

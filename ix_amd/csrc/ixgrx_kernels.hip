@@ -213,6 +213,17 @@ DEV u32x4 load16(bool ok, const uint8_t* addr, const uint8_t* dummy) {
   return *reinterpret_cast<const u32x4_a4*>(ok ? addr : dummy);
 }
 
+// 64-bit wave broadcasts (the builtins return int: each half is taken as
+// uint32_t, or a low word >= 2^31 would sign-extend over the high one)
+DEV uint64_t rfl64(uint64_t x) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+DEV uint64_t rl64(uint64_t x, uint32_t lane) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)x, lane) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), lane) << 32);
+}
+
 struct Rec {
   uint32_t w0, w1, w2, w3;  // the 16-byte ixg_rx_rec as four dwords
 };
@@ -253,6 +264,7 @@ DEV uint32_t eth_type(const uint32_t (&d)[N], uint32_t L) {
 }
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
 // The combined Toeplitz / CRC-32C byte tables (DESIGN.md "hash tables"),
@@ -1922,6 +1934,323 @@ ixg_rx_fastc_tcpx_s(KParams p) {
   fastc_loop<false, true, true>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
 }
 
+
+// ---- the flat long walk (C3: packed frames of every length) -----------------
+// The long kernel's walk over chunks whose 64 frames lie in one span of at
+// most kFlatRows KiB, in ascending order (packed batches: IMIX). Instead of a
+// prefix pass per frame and tail rounds per segment (a chain of 3-4 round
+// trips per chunk, with the wave's loads in flight only during the rounds),
+// the wave streams the chunk's whole span [A, A + nb) as rows of 1 KiB (one
+// fully coalesced 16-byte load per lane per row, all rows issued at once,
+// raw buffer loads bounded to the span: rows past it read nothing). Every
+// 16-byte piece's one's complement
+// sum goes to LDS; a lane-blocked scan turns them into prefix sums P over
+// the span (lane t's 32 pieces hold their sums from the lane's first piece,
+// E[t] the sum of everything before that), and a frame's tail [96, seg_end)
+// is P(E) - P(S) (one's complement subtraction: add the complement), each P
+// completed inside its piece: S's from the prefix dwords in registers (frame
+// starts are 4-aligned, so S = F + 96 is too), E's from the frame's end
+// piece. The prefixes (bytes 0..95, transposed: wave instruction t fetches
+// pieces 64t..64t+63 of the frame-major list) and the end pieces are copied
+// into LDS with global_load_lds right behind the span's rows, so they hit
+// the lines the rows bring into L2 and hold no registers: every frame byte is
+// fetched from HBM once. tools/probe_c3.hip read C3's spans at 5.3-5.6 TB/s
+// this way (one chunk per step, the next in flight) against 4.5 TB/s for the
+// per-segment rounds.
+// The rows (120 VGPRs) are live only while no parse state is: 256 VGPRs, two
+// waves per SIMD, 8-wave blocks whose span buffers fill the CU's LDS.
+// A chunk that is not flat (span over kFlatRows KiB, frames out of order)
+// takes flat_fallback (per-lane prefixes and tails, 8 pieces in flight).
+constexpr uint32_t kFlatRows = 30;                 // the largest span taken: 30 KiB (rows + parse in 256 VGPRs)
+constexpr uint32_t kFlatPieces = 64u * kFlatRows;  // its 16-byte pieces
+// S[] holds piece q at q + q / 32: the lane-blocked scan (lane t: pieces
+// 32t .. 32t + 31) then reads and writes conflict-free; it covers 64 blocks
+// of 32 pieces whatever the span (lanes past the span scan garbage, in bounds)
+constexpr uint32_t kFlatS = 64u * 33u;
+static_assert(kFlatPieces <= 64u * 32u, "the scan's 64 lane blocks cover the span");
+DEV uint32_t sidx(uint32_t q) { return q + (q >> 5); }
+
+struct FlatLds {
+  lds_u32* S;      // [kFlatS] piece sums, then each lane block's inclusive sums
+  lds_u32* E;      // [64] the sum before each lane block
+  lds_u32* xch;    // [64 * 4] the chunk's frames {offset lo, hi, L, -} for the copies
+  lds_u32* pre[2]; // [64 * kPrefixDw] prefixes, frame-major (DMA), per row set
+  lds_u32* ve[2];  // [64 * 4] end pieces (DMA), per row set
+};
+
+struct FlatPlan {
+  uint64_t A;   // span base (16-aligned, relative to p.base)
+  uint32_t nb;  // span bytes, a multiple of 16; 0: not flat (or no chunk)
+};
+
+// Is chunk c flat (wave-uniform)? Frames ascending: lane 0's start is the
+// span's base and the last frame's end its end, every frame inside.
+DEV FlatPlan flat_plan(const KParams& p, uint32_t c, const GDesc& g, int lane) {
+  FlatPlan f{0, 0};
+  if (c == kNoChunk) return f;
+  const uint32_t i = c * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t rest = p.n - c * 64u - 1u;
+  const uint32_t last = rest < 63u ? rest : 63u;  // the chunk's last frame's lane (wave-uniform)
+  const uint64_t A = rfl64(g.off) & ~15ull;
+  const uint64_t end = g.off + g.L;
+  const uint64_t e = rl64(end, last);
+  const bool ok = !valid || g.L == 0u || (g.off >= A && end <= e);
+  if (!wave_all(ok) || e < A || e - A > 16ull * kFlatPieces) return f;
+  f.A = A;
+  f.nb = (uint32_t)((e - A + 15u) & ~15ull);  // (the last piece: inside the batch's tail pad)
+  return f;
+}
+
+// the span's rows, all issued (a chunk that is not flat reads nothing)
+DEV void flat_rows(const KParams& p, const FlatPlan& f, int lane, u32x4 (&v)[kFlatRows]) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc(f.nb ? p.base + f.A : p.zero, f.nb);
+#pragma unroll
+  for (int r = 0; r < (int)kFlatRows; r++)
+    // (one lane offset for all rows: the row's 4 KiB group in the scalar
+    // offset, its 1 KiB within the group in the instruction's immediate)
+    v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, 16 * lane + 1024 * (r & 3), 4096 * (r >> 2), 0);
+}
+
+// The prefixes (6 pieces per frame, pieces at or past L from the zero page)
+// and the end pieces, HBM/L2 -> LDS (pre, ve); always 7 copies per lane
+// (static vmcnt): a chunk that is not flat copies the zero page. The frames'
+// offsets and lengths reach the lanes that copy their pieces through xch.
+DEV void flat_dma(const KParams& p, const FlatPlan& f, const GDesc& g, int lane0, lds_u32* xch, lds_u32* pre,
+                  lds_u32* ve) {
+  // (the lane's per-copy frame and piece are recomputed per chunk, not held
+  // across the walk in registers)
+  uint32_t lane = (uint32_t)lane0;
+  asm volatile("" : "+v"(lane));
+  xch[4 * lane] = (uint32_t)g.off;
+  xch[4 * lane + 1] = (uint32_t)(g.off >> 32);
+  xch[4 * lane + 2] = g.L;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int t = 0; t < 6; t++) {
+    const uint32_t q = 64u * (uint32_t)t + (uint32_t)lane, fr = q / 6u, j = q - 6u * fr;
+    const u32x4 x = *(const lds_u32x4*)(xch + 4u * fr);
+    const uint64_t fo = ((uint64_t)x.y << 32) | x.x;
+    const uint8_t* src = f.nb && 16u * j < x.z ? p.base + fo + 16u * j : p.zero + 16 * lane;
+    __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(pre + 256u * t), 16,
+                                     0, 0);
+  }
+  // (xch may be the end pieces' buffer: every lane has read it)
+  __builtin_amdgcn_s_waitcnt(kLdsWait);
+  __builtin_amdgcn_wave_barrier();
+  // the piece holding the frame end F + L (span-relative), when the frame
+  // can have a tail (L > 96) and its end is not piece-aligned
+  const uint64_t e = g.off + g.L - f.A;
+  const uint8_t* se = f.nb && g.L > (uint32_t)kStreamBase && (e & 15u) ? p.base + f.A + (e & ~15ull)
+                                                                      : p.zero + 16 * lane;
+  __builtin_amdgcn_global_load_lds((const void*)se, (__attribute__((address_space(3))) void*)ve, 16, 0, 0);
+}
+
+// one's complement (end-around carry) sum of a piece's four dwords
+DEV uint32_t sum4(const u32x4& v) {
+  Adc a(v.x, v.y);
+  a.add(v.z);
+  a.add(v.w);
+  return a.end();
+}
+
+// inclusive one's complement scan across the wave (DPP: row shifts, then the
+// row broadcasts; lanes with no source add 0)
+template <int CTRL, int ROWS>
+DEV uint32_t dpp_add1c(uint32_t t) {
+  return add1c(t, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t, CTRL, ROWS, 0xf, false));
+}
+DEV uint32_t wave_scan1c(uint32_t t) {
+  t = dpp_add1c<0x111, 0xf>(t);  // row_shr:1
+  t = dpp_add1c<0x112, 0xf>(t);  // row_shr:2
+  t = dpp_add1c<0x114, 0xf>(t);  // row_shr:4
+  t = dpp_add1c<0x118, 0xf>(t);  // row_shr:8
+  t = dpp_add1c<0x142, 0xa>(t);  // row_bcast:15 (rows 1, 3)
+  t = dpp_add1c<0x143, 0xc>(t);  // row_bcast:31 (rows 2, 3)
+  return t;
+}
+
+// rows -> piece sums (S): the rows' registers are free after this
+DEV void flat_sums(const FlatPlan& f, const u32x4 (&v)[kFlatRows], int lane, const FlatLds& fl) {
+  // piece 64r + lane sits at 66r + lane + lane / 32 (sidx): one lane base,
+  // the row in the instructions' immediate offsets
+  lds_u32* s0 = fl.S + (uint32_t)lane + ((uint32_t)lane >> 5);
+#pragma unroll
+  for (int r = 0; r < (int)kFlatRows; r++)
+    if (1024u * (uint32_t)r < f.nb) s0[66 * r] = sum4(v[r]);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// piece sums -> per lane block inclusive sums (S) and block bases (E)
+DEV void flat_blocks(int lane, const FlatLds& fl) {
+  // lane t: pieces 32t .. 32t + 31 (past the span: garbage, never read back)
+  lds_u32* b = fl.S + 33u * (uint32_t)lane;
+  uint32_t x[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) x[k] = b[k];
+#pragma unroll
+  for (int k = 1; k < 32; k++) x[k] = add1c(x[k - 1], x[k]);
+#pragma unroll
+  for (int k = 0; k < 32; k++) b[k] = x[k];
+  // the sum before each block: exclusive scan of the blocks' totals
+  const uint32_t incl = wave_scan1c(x[31]);
+  fl.E[lane] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x138, 0xf, 0xf, false);  // wave_shr:1
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// P at span position x (bytes [0, x) of the span): P of the pieces before
+// x's piece plus `part`, the bytes of x's piece before x
+DEV uint32_t flat_p(const FlatLds& fl, uint32_t x, uint32_t part) {
+  const uint32_t q = x >> 4;
+  const uint32_t pq = q ? add1c(fl.S[sidx(q - 1u)], fl.E[(q - 1u) >> 5]) : 0u;
+  return add1c(pq, part);
+}
+
+// chunk c's records from its staged (masked) prefixes and the span's P;
+// SHAPE: kShapeFixed for a wave of IPv4 ihl 5 frames, else kShapeAny
+template <int SHAPE, bool DMX>
+DEV void flat_finish(const KParams& p, const uint64_t* __restrict__ T, uint32_t c, int lane, const WaveLds& w,
+                     const FlatLds& fl, const FlatPlan& f, const GDesc& g, const uint32_t (&d)[kPrefixDw],
+                     const u32x4& ve) {
+  const uint32_t i = c * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t L = g.L;
+  LaneState s;
+  lane_parse<SHAPE, kPrefixDw>(p, Tab64{T}, d, L, s, w.t6);
+  uint32_t res = l4_residual(s);
+  const bool strm = valid && s.stream;
+  if (wave_any(strm)) {
+    const uint32_t rf = (uint32_t)(g.off - f.A);  // the frame's start in the span (4-aligned)
+    // S = F + 96: its piece's bytes before S are prefix dwords 24 - k .. 23
+    const uint32_t ks = (rf & 15u) >> 2;
+    const uint32_t ps = add1c(ks >= 3u ? d[21] : 0u, add1c(ks >= 2u ? d[22] : 0u, ks >= 1u ? d[23] : 0u));
+    const uint32_t pS = flat_p(fl, rf + (uint32_t)kStreamBase, ps);
+    // E = F + seg_end: its piece, masked (the end piece staged for E = F + L;
+    // a segment ending short of the frame in another piece loads its own)
+    const uint32_t re = rf + s.seg_end;
+    u32x4 v = ve;
+    const bool other = strm && (re & ~15u) != ((rf + L) & ~15u);
+    if (wave_any(other) && other) v = load16(true, p.base + f.A + (re & ~15u), p.zero);
+    const uint32_t pE = flat_p(fl, re, sum4(mask_piece(v, (int)(re & 15u))));
+    uint32_t tail = add1c(pE, ~pS);
+    // x - x is the negative zero 0xffffffff: exact for a non-zero tail sum,
+    // but a tail of zero bytes sums to 0 (ICMP, with no pseudo header, can
+    // tell the two apart): such lanes sum their tail exactly (rare)
+    const bool amb = strm && tail == 0xffffffffu;
+    if (wave_any(amb) && amb) tail = span_sum(p, g.off, (uint32_t)kStreamBase, s.seg_end);
+    if (strm) res = (~fold16(add1c(fold32(s.l4_acc), tail))) & 0xffffu;
+  }
+  if (!valid) return;
+  const Rec r = make_record(p, d, L, s, res);
+  store_record(p, i, r, s.ip_res, res);
+  store_demux<DMX>(p, i, r, s.src, s.dst, s.ports);
+}
+
+// A chunk the flat walk does not take (its span over kFlatRows KiB, or its
+// frames out of order; rare in packed batches of IX frames): per-lane
+// prefix loads, the general parse, and each tail [96, seg_end) summed by its
+// own lane, 8 pieces in flight (slow_chunk's path with the loads batched).
+// Registers stay within the flat path's own (no streaming rounds).
+DEV uint32_t tail_sum8(const KParams& p, uint64_t off, uint32_t a, uint32_t e) {
+  uint32_t s = 0;
+  for (uint32_t pos = a; wave_any(pos < e); pos += 128u) {
+    u32x4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) v[k] = load16(pos + 16u * k < e, p.base + off + pos + 16u * k, p.zero);
+#pragma unroll
+    for (int k = 0; k < 8; k++) s = add1c(s, sum4(mask_piece(v[k], (int)e - (int)(pos + 16u * k))));
+  }
+  return s;
+}
+template <bool DMX>
+DEV void flat_fallback(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, uint32_t c, int lane,
+                       const GDesc& g) {
+  GPre x;
+  gen_pre<false, false>(p, g, lane, x);
+  const uint32_t i = c * 64u + (uint32_t)lane;
+  const bool valid = i < p.n;
+  const uint32_t L = g.L;
+  uint32_t d[kPrefixDw];
+#pragma unroll
+  for (int k = 0; k < kPrefixDw; k++) d[k] = x.d[k];
+  mask_prefix(d, L);
+  LaneState s;
+  lane_parse<kShapeAny, kPrefixDw>(p, Tab64{T}, d, L, s, w.t6);
+  uint32_t res = l4_residual(s);
+  const bool strm = valid && s.stream;
+  if (wave_any(strm)) {
+    const uint32_t t = tail_sum8(p, g.off, (uint32_t)kStreamBase, strm ? s.seg_end : 0u);
+    if (strm) res = (~fold16(add1c(fold32(s.l4_acc), t))) & 0xffffu;
+  }
+  if (!valid) return;
+  const Rec r = make_record(p, d, L, s, res);
+  store_record(p, i, r, s.ip_res, res);
+  store_demux<DMX>(p, i, r, s.src, s.dst, s.ports);
+}
+
+// The walk. Per chunk: its rows and staging copies, then its descriptors'
+// successor, then (rows landed) the scan, the staged prefixes and the parse.
+// The rows are in flight while no parse state is live, so a wave fits in
+// 256 VGPRs and two waves share a SIMD: one parses while the other waits on
+// its rows. (Pipelined one chunk deep instead -- chunk j+1's rows in flight
+// during chunk j's parse -- the rows and the parse do not fit 256 VGPRs
+// together: 30 rows spill two of them, C3 1.482 ms; 28 rows, spill-free,
+// 1.403 ms; this walk 1.335 ms, same process, profiles/r06/flat/.)
+template <bool OFFS, int SM, bool DMX>
+DEV void flat_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLds& w, const FlatLds& fl,
+                   const lds_u32* q, uint32_t nq, int lane0, GDesc D0) {
+  for (uint32_t j = 0; j < nq; j++) {
+    // the lane index laundered per chunk: everything derived from it
+    // (addresses, masks) is recomputed here instead of being held in
+    // registers across the walk, which the rows need
+    int lane = lane0;
+    asm volatile("" : "+v"(lane));
+    const uint32_t c = q[j];
+    const FlatPlan F = flat_plan(p, c, D0, lane);
+    u32x4 R[kFlatRows];
+    if (F.nb) {
+      flat_rows(p, F, lane, R);
+      flat_dma(p, F, D0, lane, fl.xch, fl.pre[0], fl.ve[0]);
+    }
+    GDesc D1;
+    gen_desc<OFFS>(p, j + 1 < nq ? q[j + 1] : kNoChunk, lane, D1);
+    if (F.nb) {
+      flat_sums(F, R, lane, fl);
+      flat_blocks(lane, fl);
+      __builtin_amdgcn_s_waitcnt(kGldsWait);
+      __builtin_amdgcn_wave_barrier();
+      uint32_t d[kPrefixDw];
+      const lds_u32* row = fl.pre[0] + (uint32_t)lane * kPrefixDw;
+      d[0] = d[1] = d[2] = 0;  // MAC addresses: never read
+      d[3] = row[3];
+#pragma unroll
+      for (int k = 1; k < 6; k++) {
+        const u32x4 v = *(const lds_u32x4*)(row + 4 * k);
+        d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+      }
+      const u32x4 ve = *(const lds_u32x4*)(fl.ve[0] + 4u * (uint32_t)lane);
+      mask_prefix(d, D0.L);
+      if (wave_all(c * 64u + (uint32_t)lane >= p.n || (eth_type(d, D0.L) == 0x0800u && byte_at(d, 14) == 0x45u)))
+        flat_finish<kShapeFixed, DMX>(p, T, c, lane, w, fl, F, D0, d, ve);
+      else
+        flat_finish<kShapeAny, DMX>(p, T, c, lane, w, fl, F, D0, d, ve);
+    } else {
+      // not flat: each lane its own tail
+      flat_fallback<DMX>(p, T, w, c, lane, D0);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    D0 = D1;
+  }
+}
+
 // ---- general kernel --------------------------------------------------------
 // Every header shape the reference handles. Waves scan the defer flags 64
 // chunks at a time and process the flagged chunks (all chunks when
@@ -1972,12 +2301,19 @@ DEV bool gen_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveLd
 // fixed-shape kernel deferred as short or, in IXG_MODE_SHORT, walks every
 // chunk and defers the long ones itself. IXG_CLS_LONG: everything; the
 // deferred long chunks, or every chunk (p.defer null, or IXG_MODE_LONG).
+// FLAT: chunk lists in long mode take flat_walk (8-wave blocks, no IPv6
+// tables: its span buffers use the LDS they would need)
 template <bool OFFS, uint32_t CLS, bool SEARLY = true, int SM = 0, bool LATE = false, bool BIGOK = true,
-          int kWaves = 4, int kQGroups = 4, bool DMX = true>
+          int kWaves = 4, int kQGroups = 4, bool DMX = true, bool FLAT = false>
 DEV void general_body(const KParams& p) {
   __shared__ uint64_t T[12 * 256];
-  __shared__ uint32_t sh_list[kWaves][64], sh_end[kWaves][64], sh_offlo[kWaves][64], sh_offhi[kWaves][64],
-      sh_sum[kWaves][64], sh_q[kWaves][64 * kQGroups];
+  // (FLAT: the span sums; the per-segment path's lists live in them, and
+  // the frames' exchange for the staging copies in the end pieces' buffer)
+  constexpr int kFw = FLAT ? kWaves : 1;
+  __shared__ uint32_t sh_S[kFw][FLAT ? kFlatS : 1], sh_E[kFw][FLAT ? 64 : 1], sh_ve[kFw][FLAT ? 256 : 1];
+  constexpr int kLw = FLAT ? 1 : kWaves;
+  __shared__ uint32_t sh_list[kLw][64], sh_end[kLw][64], sh_offlo[kLw][64], sh_offhi[kLw][64], sh_sum[kLw][64],
+      sh_q[kWaves][64 * kQGroups];
   // the big-chunk prefix stash (not in the short kernel: no big chunks there)
   constexpr int kPre = CLS == IXG_CLS_SHORT ? 1 : 64 * kPrefixDw;
   __shared__ uint32_t sh_pre[kWaves][kPre];
@@ -2011,9 +2347,12 @@ DEV void general_body(const KParams& p) {
     for (int k = threadIdx.x; k < (int)IXG_TAB6_WORDS / 4; k += 64 * kWaves) dyn6[k] = reinterpret_cast<const u32x4*>(p.tab6)[k];
   }
   stage_tables(p, T);
-  const WaveLds w{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
-                  LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6),
-                  LDS(lds_u32, sh_pre[wave])};
+  lds_u32* lists = FLAT ? LDS(lds_u32, sh_S[FLAT ? wave : 0]) : nullptr;
+  const WaveLds w = FLAT ? WaveLds{lists, lists + 64, lists + 128, lists + 192, lists + 256, LDS(const lds_u32, dyn6),
+                                   LDS(lds_u32, sh_pre[wave])}
+                         : WaveLds{LDS(lds_u32, sh_list[wave]), LDS(lds_u32, sh_end[wave]), LDS(lds_u32, sh_offlo[wave]),
+                                   LDS(lds_u32, sh_offhi[wave]), LDS(lds_u32, sh_sum[wave]), LDS(const lds_u32, dyn6),
+                                   LDS(lds_u32, sh_pre[wave])};
   lds_u32* q = LDS(lds_u32, sh_q[wave]);
   bool seen = false;
   // groups g0, g0+nw, ... of this wave, kQGroups at a time: their deferred
@@ -2050,6 +2389,13 @@ DEV void general_body(const KParams& p) {
     gen_desc<OFFS>(p, q[0], lane, D0);
     if (CLS == IXG_CLS_SHORT)
       seen |= gen_walk<OFFS, SEARLY, kModeFirst, 0, false, true, DMX>(p, T, w, q, nq, lane, D0);
+    else if (FLAT && !launch_big(p))
+      flat_walk<OFFS, SM, DMX>(p, T, w,
+                               FlatLds{LDS(lds_u32, sh_S[FLAT ? wave : 0]), LDS(lds_u32, sh_E[FLAT ? wave : 0]),
+                                       LDS(lds_u32, sh_ve[FLAT ? wave : 0]),
+                                       {LDS(lds_u32, sh_pre[wave]), LDS(lds_u32, sh_pre[wave])},
+                                       {LDS(lds_u32, sh_ve[FLAT ? wave : 0]), LDS(lds_u32, sh_ve[FLAT ? wave : 0])}},
+                               q, nq, lane, D0);
     else if (!SEARLY || wave_any(D0.L > (uint32_t)kStreamBase + 32u))
       gen_walk<OFFS, false, kModeLong, SM, LATE, BIGOK, DMX>(p, T, w, q, nq, lane, D0);
     else
@@ -2072,6 +2418,10 @@ DEV void general_body(const KParams& p) {
 // A/B, and C3's FETCH_SIZE 6.64 -> 6.53 GB)
 IXG_GEN_KERNEL(ixg_rx_general_s, false, IXG_CLS_LONG, 2, true, 1)
 IXG_GEN_KERNEL(ixg_rx_general_o, true, IXG_CLS_LONG, 2, true, 1)
+// the long kernel with the flat walk (8-wave blocks sharing one table copy:
+// the 8 waves' span buffers fill the CU's LDS); not under IXG_F_IPV6
+IXG_GENW_KERNEL(ixg_rx_glong_s, 8, false, IXG_CLS_LONG, 2, false, 1, false, true, 8, 1, true, true)
+IXG_GENW_KERNEL(ixg_rx_glong_o, 8, true, IXG_CLS_LONG, 2, false, 1, false, true, 8, 1, true, true)
 // the short-class general kernel (no streaming rounds): 4 waves/SIMD
 // without the one-ahead prefix prefetch (128 VGPRs; C5 -3% against the
 // 3-wave prefetching build)
@@ -2098,16 +2448,6 @@ IXG_GENW_KERNEL(ixg_rx_short_w8d_o, 8, true, IXG_CLS_SHORT, 4, false, 0, false, 
 constexpr uint32_t kSpanMax = 6144;             // bytes per wave's span buffer
 constexpr int kSpanWaves = 16;                  // 1024-thread blocks, 1 per CU
 
-// 64-bit wave broadcasts (the builtins return int: each half is taken as
-// uint32_t, or a low word >= 2^31 would sign-extend over the high one)
-DEV uint64_t rfl64(uint64_t x) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
-         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
-}
-DEV uint64_t rl64(uint64_t x, uint32_t lane) {
-  return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)x, lane) |
-         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(x >> 32), lane) << 32);
-}
 
 // A chunk's span: LDS image of [base, base + 1024 * npc) (npc = 0: not
 // span-contiguous, load per lane)
@@ -2378,8 +2718,17 @@ static uint32_t grid_for(kern_fn k, uint64_t want, uint32_t ncu, size_t shmem = 
 // reflected mbuf byte of multi-batch runs after polling the word, in DIRECT
 // and copy modes (tests/test_async.py, tests/test_icmp.py async tests,
 // tests/test_integration_example.py).
+// The word is the first of four: f[2..3] get the device's wall clock
+// (wall_clock64, constant rate) when the stamp runs, stored before the
+// release, so the host can tell how late it saw a finished batch
+// (ixg_rx_async_stats' worst-batch split).
 extern "C" __global__ void __launch_bounds__(64) ixg_done_stamp(uint32_t* f, uint32_t v) {
-  if (threadIdx.x == 0) __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {
+    const uint64_t t = wall_clock64();
+    f[2] = (uint32_t)t;
+    f[3] = (uint32_t)(t >> 32);
+    __hip_atomic_store(f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 extern "C" int ixgrx_stamp(uint32_t* flag, uint32_t v, void* stream) {
@@ -2460,6 +2809,16 @@ extern "C" int ixgrx_launch(const void* params, uint32_t ncu, void* stream) {
     ps.self_sample = self ? 1u : 0u;
     hipLaunchKernelGGL(ks.k[lay], dim3(grid_for(ks.k[lay], want, ncu, sh6, ks.block)), dim3(ks.block), sh6,
                        (hipStream_t)stream, ps);
+  }
+  // the flat walk's build (8-wave blocks) unless the IPv6 tables need the LDS,
+  // or a fixed stride puts every chunk's span over kFlatRows KiB (C4: the
+  // general kernel's big-chunk walk, glong's build of it is ~1 % slower)
+  static const kern_fn k_glong[2] = {ixg_rx_glong_s, ixg_rx_glong_o};
+  if (!p.tab6 && !p.host_mem && (p.off || 63ull * p.stride < 16ull * kFlatPieces)) {
+    const kern_fn kg = k_glong[lay];
+    const uint64_t gb8 = ((nchunks + 63u) / 64u + 7u) / 8u;
+    hipLaunchKernelGGL(kg, dim3(grid_for(kg, gb8, ncu, 0, 512)), dim3(512), 0, (hipStream_t)stream, p);
+    return (int)hipGetLastError();
   }
   const kern_fn kg = k_gen[lay];
   hipLaunchKernelGGL(kg, dim3(grid_for(kg, p.host_mem ? wave_blocks : group_blocks, ncu, sh6)), dim3(kBlock), sh6,

@@ -17,7 +17,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libixgrx.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 IXG_F_NO_CSUM_DROP = 1 << 0
 IXG_F_IPV6 = 1 << 1
 IXG_TAIL_PAD = 64
@@ -82,7 +82,9 @@ class AsyncStats(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint64) for k in (
         "frames_submitted", "frames_returned", "frames_refused", "submit_calls", "poll_calls", "batches",
         "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns", "launch_max_ns",
-        "image_bytes", "inplace_bytes", "frames_launched")]
+        "image_bytes", "inplace_bytes", "frames_launched",
+        "worst_total_ns", "worst_open_ns", "worst_gpu_ns", "worst_visible_ns", "worst_returned_ns",
+        "worst_wait_ns", "worst_outside_ns")]
 
 
 IXG_ASYNC_DIRECT = 1 << 0

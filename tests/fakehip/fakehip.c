@@ -250,6 +250,14 @@ static struct op *new_op(int kind)
 
 /* ---- the runtime (every entry point under g_mu) ------------------------- */
 hipError_t hipSetDevice(int d) { return d == 0 ? hipSuccess : hipErrorInvalidDevice; }
+/* (no device clock here: the stats' worst-batch split reports no device time) */
+hipError_t hipDeviceGetAttribute(int *v, hipDeviceAttribute_t a, int d)
+{
+	(void)a;
+	(void)d;
+	*v = 0;
+	return hipErrorNotSupported;
+}
 hipError_t hipGetDeviceCount(int *n)
 {
 	*n = 1;

@@ -383,3 +383,29 @@ def test_not_staged_bytes_are_not_read(kind, cfg):
         eng.close()
     assert np.array_equal(m, ptrs)
     assert np.array_equal(r.view(np.uint8).reshape(-1, 16), exp)
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_worst_batch_split(direct):
+    """ixg_rx_async_stats splits the worst batch's time
+    into open (gather -> launch), gpu (launch -> the completion stamp ran, by
+    the device's wall clock calibrated at async_init), visible (stamp -> the
+    library saw the word) and returned (seen -> last frame polled); the parts
+    add up to the total, and a batch that ran on the device has a device
+    part. Records still against the oracle."""
+    tr, arena, ptrs = _mbufs("imix", 20000, seed=0x5B1)
+    rng = np.random.default_rng(0x5B1)
+    eng = ixgrx.RxEngine(ixgrx.Config(KEY))
+    try:
+        eng.async_init(**{**ixgrx.ASYNC_DEFAULTS, "direct": direct})
+        eng.async_stats(reset=True)
+        m, r = _run_loop(eng, ptrs, rng)
+        st = eng.async_stats()
+    finally:
+        eng.close()
+    assert np.array_equal(m, ptrs)
+    assert np.array_equal(r.view(np.uint8).reshape(-1, 16), oracle.rx_mbufs(KEY, 128, 0, 0, ptrs, threads=8))
+    parts = st["worst_open_ns"] + st["worst_gpu_ns"] + st["worst_visible_ns"] + st["worst_returned_ns"]
+    assert st["worst_total_ns"] > 0 and parts == st["worst_total_ns"], st
+    assert st["worst_gpu_ns"] > 0, st          # the device clock was read and calibrated
+    assert st["worst_wait_ns"] <= st["worst_total_ns"]

@@ -445,7 +445,13 @@ def test_async_stats_counters(fake):
         st = eng.async_stats(reset=True)
         assert st["frames_returned"] == 300 and st["batches"] == 3 and st["batches_by_time"] == 1
         assert st["gather_ns"] > 0 and st["launch_ns"] > 0 and st["poll_calls"] >= 3
+        # the worst batch's split: the parts add up to
+        # the total; no device clock on the fake runtime, so no "gpu" part
+        assert st["worst_total_ns"] > 0 and st["worst_gpu_ns"] == 0
+        assert st["worst_open_ns"] + st["worst_visible_ns"] + st["worst_returned_ns"] == st["worst_total_ns"]
+        assert st["worst_wait_ns"] <= st["worst_total_ns"]
         assert eng.async_stats()["frames_submitted"] == 0   # reset
+        assert eng.async_stats()["worst_total_ns"] == 0
     finally:
         eng.close()
     assert np.array_equal(np.concatenate([m, m3]), ptrs[:300])

@@ -35,7 +35,18 @@ def main():
     wl = bench.Workload(args.workload, seed=0x1B0002, dev=dev)
     engs = {}
     splits = args.splits.split(",") if args.splits else ["general" if args.general else "auto"]
+    import ctypes
     for path in re.split("[,+]", args.libs):
+        # builds of older revisions may carry an older ABI version; the A/B
+        # only calls the RX entry points, which have not changed
+        full = os.path.join(ROOT, path)
+        v = ctypes.CDLL(full).ixg_abi_version()
+        if v != ixgrx.ABI_VERSION:
+            cur, ixgrx.ABI_VERSION = ixgrx.ABI_VERSION, v
+            try:
+                ixgrx.load_library(full)
+            finally:
+                ixgrx.ABI_VERSION = cur
         for sp in splits:
             name = os.path.basename(path) + ("" if len(splits) == 1 else ":" + sp)
             engs[name] = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags),

@@ -9,7 +9,13 @@ from ix_amd import ixgrx, traces
 lib, w = sys.argv[1], sys.argv[2]
 n = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 wl = bench.Workload(w, seed=0x1B0002, dev=torch.device("cuda:0"))
-e = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags), lib_path=os.path.join(ROOT, lib))
+import ctypes
+full = os.path.join(ROOT, lib)
+v = ctypes.CDLL(full).ixg_abi_version()  # (a build of an older revision: its own ABI version)
+cur, ixgrx.ABI_VERSION = ixgrx.ABI_VERSION, v
+ixgrx.load_library(full)
+ixgrx.ABI_VERSION = cur
+e = ixgrx.RxEngine(ixgrx.Config(traces.RSS_KEY, flags=wl.flags), lib_path=full)
 s = torch.cuda.current_stream()
 for _ in range(n):
     wl.launch(e, s.cuda_stream)

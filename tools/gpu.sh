@@ -58,6 +58,11 @@ for STEP in "$@"; do
       timeout -k 10 120 rocprofv3 --pmc $P1 --output-format csv -d "$d/${w}_p1" -o p -- python3 tools/dbg/run_lib.py "$lib" "$w" > "$d/p1.log" 2>&1 &&
       timeout -k 10 120 rocprofv3 --pmc $P2 --output-format csv -d "$d/${w}_p2" -o p -- python3 tools/dbg/run_lib.py "$lib" "$w" > "$d/p2.log" 2>&1 &&
       python3 tools/sq_report.py "$d" "$w" > "$O/sqlib_$i.txt" ;;
+    pmclib)
+      # pmclib:W:LIB:C1+C2+... one counter pass of one workload through a library build
+      w=${arg%%:*}; r=${arg#*:}; lib=${r%%:*}; cs=${r#*:}; d="$O/pmclib_$i"; mkdir -p "$d"
+      timeout -k 10 120 rocprofv3 --pmc ${cs//+/ } --output-format csv -d "$d/${w}_p1" -o p -- python3 tools/dbg/run_lib.py "$lib" "$w" > "$d/p1.log" 2>&1 &&
+      python3 tools/sq_report.py "$d" "$w" > "$O/pmclib_$i.txt" ;;
     *) echo "unknown step $STEP"; exit 2 ;;
   esac
   rc=$?
