@@ -1130,13 +1130,15 @@ def summary(res: dict) -> dict:
         top = max((k for k in lp if k.startswith("threads") and k[7:].isdigit()), key=lambda k: int(k[7:]), default=None)
         if top:
             out["host_path"]["t%s_max_latency_us" % top[7:]] = lp[top].get("latency_us", {}).get("max")
-        # the worst batch of the zero-copy line, split where its time went
-        # (ixg_rx_async_stats: open / gpu / visible / returned; wait, outside)
+        # the worst batch of the 16-thread and zero-copy lines, split where its
+        # time went (ixg_rx_async_stats: open / gpu / visible / returned; wait,
+        # outside; poll(wait)'s naps and the longest)
+        keys = ("total", "open", "gpu", "visible", "returned", "wait", "outside", "naps", "nap_max")
         zc = next((k for k in lp if k.endswith("_zero_copy")), None)
-        if zc and "worst_batch_us" in lp[zc]:
-            w = lp[zc]["worst_batch_us"]
-            out["host_path"]["zc_worst_us"] = {k: w[k] for k in ("total", "open", "gpu", "visible", "returned",
-                                                                  "outside") if k in w}
+        for name, k in (("t%s_worst_us" % top[7:] if top else None, top), ("zc_worst_us", zc)):
+            if name and k and "worst_batch_us" in lp[k]:
+                w = lp[k]["worst_batch_us"]
+                out["host_path"][name] = {x: w[x] for x in keys if x in w}
         out["host_path"]["parity"] = hp.get("parity")
     if "cpu_baseline" in res:
         out["cpu_baseline_mpps"] = res["cpu_baseline"]["value"]

@@ -424,11 +424,15 @@ static int run_loop(void)
 	/* the worst batch of all threads, and where its time went */
 	const struct ixg_rx_async_stats *wb = &ws[0].ast;
 	int wth = 0;
-	for (int i = 0; i < opt.threads; i++)
+	double nap_max = 0;
+	for (int i = 0; i < opt.threads; i++) {
 		if (ws[i].ast.worst_total_ns > wb->worst_total_ns) {
 			wb = &ws[i].ast;
 			wth = i;
 		}
+		if ((double)ws[i].ast.nap_max_ns > nap_max)
+			nap_max = (double)ws[i].ast.nap_max_ns;
+	}
 	for (int i = 0; i < opt.threads; i++) {
 		const struct ixg_rx_async_stats *a = &ws[i].ast;
 		g_ns += (double)a->gather_ns;
@@ -476,7 +480,8 @@ static int run_loop(void)
 	       "\"frames_per_batch\": %.0f, \"batches_by_time\": %.3f, \"refused_share\": %.3f, "
 	       "\"max_loop_gap_us\": %.1f, \"max_launch_us\": %.1f, \"context_switches\": {\"voluntary\": %ld, \"involuntary\": %ld}}, "
 	       "\"worst_batch_us\": {\"thread\": %d, \"total\": %.1f, \"open\": %.1f, \"gpu\": %.1f, \"visible\": %.1f, "
-	       "\"returned\": %.1f, \"wait\": %.1f, \"outside\": %.1f, \"thread_max_loop_gap\": %.1f}}\n",
+	       "\"returned\": %.1f, \"wait\": %.1f, \"outside\": %.1f, \"thread_max_loop_gap\": %.1f, \"naps\": %llu, "
+	       "\"nap_max\": %.1f, \"all_threads_nap_max\": %.1f}}\n",
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
 	       nl ? lat[nl - 1] : 0.0, nl, staged_b, inplace_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
@@ -487,7 +492,8 @@ static int run_loop(void)
 	       batches ? fr / (double)batches : 0.0, batches ? (double)by_time / (double)batches : 0.0,
 	       offered ? (double)refused / (double)offered : 0.0, gap * 1e6, lmax / 1e3, vcs, ivcs, wth,
 	       wb->worst_total_ns / 1e3, wb->worst_open_ns / 1e3, wb->worst_gpu_ns / 1e3, wb->worst_visible_ns / 1e3,
-	       wb->worst_returned_ns / 1e3, wb->worst_wait_ns / 1e3, wb->worst_outside_ns / 1e3, ws[wth].max_gap * 1e6);
+	       wb->worst_returned_ns / 1e3, wb->worst_wait_ns / 1e3, wb->worst_outside_ns / 1e3, ws[wth].max_gap * 1e6,
+	       (unsigned long long)wb->worst_naps, wb->worst_nap_max_ns / 1e3, nap_max / 1e3);
 	if (opt.dump) {
 		FILE *f = fopen(opt.dump, "wb");
 		if (!f || fwrite(ws[0].dump, sizeof(struct ixg_rx_rec), ws[0].ndump, f) != ws[0].ndump)

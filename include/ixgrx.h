@@ -282,9 +282,14 @@ struct ixg_rx_async_stats {
 	 * seen -> the last frame handed back by poll. open + gpu + visible +
 	 * returned = total. wait: time poll(wait) blocked on this batch; outside:
 	 * the longest interval between two calls into the library while the batch
-	 * was pending (the caller's own work, or the thread off its CPU). */
+	 * was pending (the caller's own work, or the thread off its CPU).
+	 * naps / nap_max: the naps poll(wait) took on it and the longest one (a
+	 * nap asks for 10 us: one of milliseconds is the thread off its CPU, many
+	 * short ones a completion word that was not there yet). */
 	uint64_t worst_total_ns, worst_open_ns, worst_gpu_ns, worst_visible_ns, worst_returned_ns;
 	uint64_t worst_wait_ns, worst_outside_ns;
+	uint64_t worst_naps, worst_nap_max_ns;
+	uint64_t nap_max_ns;       /* the longest single nap of poll(wait) in the window */
 };
 /* Copy the counters to *out (may be NULL) and, reset != 0, zero them. 0 or -errno. */
 int ixg_rx_async_stats(void *ctx, struct ixg_rx_async_stats *out, int reset);

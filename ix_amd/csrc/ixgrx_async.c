@@ -62,6 +62,7 @@ struct ixg_abatch {
 	/* where its frames' time goes (ixg_rx_async_stats' worst batch): ns */
 	uint64_t t_launch, t_seen, t_gpu, wait_ns;
 	uint64_t gap_max;    /* TSC ticks: longest interval outside the library while pending */
+	uint64_t naps, nap_max; /* poll(wait)'s naps on it, the longest (ns) */
 };
 
 struct ixg_async {
@@ -226,6 +227,8 @@ static void batch_returned(struct ixg_async *a, const struct ixg_abatch *b, uint
 	a->st.worst_returned_ns = t - b->t_seen;
 	a->st.worst_wait_ns = b->wait_ns;
 	a->st.worst_outside_ns = b->gap_max; /* (ticks: converted when read) */
+	a->st.worst_naps = b->naps;
+	a->st.worst_nap_max_ns = b->nap_max;
 }
 
 /* the library saw batch b's completion word (its stamp's device clock: when
@@ -345,7 +348,7 @@ static struct ixg_abatch *open_batch(struct ixg_async *a, uint64_t t)
 	b->nabs = b->nic = 0;
 	b->span = b->hi = b->link = 0;
 	b->dead = 0;
-	b->wait_ns = b->gap_max = 0;
+	b->wait_ns = b->gap_max = b->naps = b->nap_max = 0;
 	a->tail = (a->tail + 1) % a->cfg.depth;
 	a->count++;
 	return b;
@@ -553,7 +556,14 @@ static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, struc
 			}
 		}
 		const struct timespec nap = {0, IXG_WAIT_NAP_NS};
+		const uint64_t n0 = now_ns();
 		nanosleep(&nap, NULL);
+		const uint64_t dn = now_ns() - n0;
+		b->naps++;
+		if (dn > b->nap_max)
+			b->nap_max = dn;
+		if (dn > c->async->st.nap_max_ns)
+			c->async->st.nap_max_ns = dn;
 	}
 }
 

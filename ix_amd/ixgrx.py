@@ -84,7 +84,7 @@ class AsyncStats(ctypes.Structure):
         "batches_by_time", "gather_ns", "launch_ns", "poll_ns", "wait_ns", "launch_max_ns",
         "image_bytes", "inplace_bytes", "frames_launched",
         "worst_total_ns", "worst_open_ns", "worst_gpu_ns", "worst_visible_ns", "worst_returned_ns",
-        "worst_wait_ns", "worst_outside_ns")]
+        "worst_wait_ns", "worst_outside_ns", "worst_naps", "worst_nap_max_ns", "nap_max_ns")]
 
 
 IXG_ASYNC_DIRECT = 1 << 0

@@ -19,6 +19,9 @@ box: one JSON line per point, with the run's cgroup CPU throttling
        depth    16 threads, idle=wait: depth 2/3/4 x max_wait_us 50/100
        abbig:L1,L2,..  as ab, over 1514-B frames: staged and zero copy at
                 batch_bytes 1 MiB and 512 KiB
+       tailab:L1,L2,..  the 16-thread tail: C2 frames staged and 1514-B frames
+                zero copy, library builds interleaved over 3 rounds, with the
+                worst batch's latency split and the cgroup throttling
        ab:L1,L2,..  (or L1+L2+..) 16 threads, idle=wait, library builds interleaved over 4
                 rounds (each Li a directory holding a libixgrx.so, or
                 "default"): same-box A/B of host-path library variants
@@ -53,7 +56,8 @@ def point(path, label, env=None, **kw):
            "refused_share": b.get("refused_share"), "staged_bytes_per_frame": r.get("staged_bytes_per_frame"),
            "arena_pages": r.get("cfg", {}).get("arena_pages"),
            "throttled": s1.get("nr_throttled", 0) - s0.get("nr_throttled", 0),
-           "throttled_ms": (s1.get("throttled_usec", 0) - s0.get("throttled_usec", 0)) / 1e3, "err": r.get("error")}
+           "throttled_ms": (s1.get("throttled_usec", 0) - s0.get("throttled_usec", 0)) / 1e3,
+           "worst_batch_us": r.get("worst_batch_us"), "err": r.get("error")}
     print(json.dumps(out), flush=True)
 
 
@@ -120,6 +124,15 @@ def main():
                     env = None if lib == "default" else {"LD_LIBRARY_PATH": lib}
                     point(fb, dict(lib=lib, rep=rep, batch_bytes=bb, zero_copy=reg), env=env, threads=16,
                           seconds=sec, arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which.startswith("tailab:"):
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for rep in range(3):
+            for lib in re.split("[,+]", which[7:]):
+                env = None if lib == "default" else {"LD_LIBRARY_PATH": lib}
+                point(f, dict(lib=lib, rep=rep, frames=60), env=env, threads=16, seconds=sec, arena=1 << 17)
+                point(fb, dict(lib=lib, rep=rep, frames=1514, zero_copy=1), env=env, threads=16, seconds=sec,
+                      arena=1 << 15, register=1)
     elif which.startswith("ab:"):
         import subprocess
         libs = re.split("[,+]", which[3:])
