@@ -36,12 +36,16 @@ def kernels(wl) -> str:
     64 B the coalesced fixed-shape kernel, else the sampler and the lane-load
     one; then the short and the long general kernels (each exits at once
     when its class has nothing deferred), or behind the coalesced kernel one
-    general kernel taking both classes (ixg_rx_any_s)."""
+    general kernel taking both classes (ixg_rx_any_s). The long class runs
+    the flat walk's build (ixg_rx_glong_*) unless the IPv6 tables are staged
+    (IXG_F_IPV6) or a fixed stride can never give a flat chunk."""
+    v6 = bool(getattr(wl, "flags", 0) & 2)
     if wl.off is not None:
-        return "ixg_rx_short_sp_o (samples the launch mode itself) + ixg_rx_general_o"
+        return "ixg_rx_short_sp_o (samples the launch mode itself) + " + ("ixg_rx_general_o" if v6 else "ixg_rx_glong_o")
     if wl.stride <= 64:
         return "ixg_rx_fastc_s (deferred chunks finished in the same dispatch)"
-    return "ixg_rx_short_sp_s (samples the launch mode itself) + ixg_rx_general_s"
+    flat = not v6 and 63 * wl.stride < 30 * 1024
+    return "ixg_rx_short_sp_s (samples the launch mode itself) + " + ("ixg_rx_glong_s" if flat else "ixg_rx_general_s")
 
 
 # untimed launches before each secondary line (demux, events, TX) is timed

@@ -33,6 +33,9 @@
  *   again at once (spin). On a CPU quota (the GPU box: 16 CPUs per 100 ms),
  *   16 spinning threads plus the HIP runtime's own got the process throttled
  *   for ~10 ms at a time.
+ *   pin=K: thread i runs on the K*i-th CPU of the process's allowed set (as
+ *   IX pins one thread per dedicated core, dp/core/cpu.c); 0 (the default):
+ *   the scheduler places the threads
  * FRAMES_FILE: u32 count, u16 lengths[count], then the frames back to back.
  * dump=FILE (loop mode): thread 0's first `count` records, in submission
  * order, for the caller's parity check against the oracle.
@@ -41,6 +44,7 @@
 #include <execinfo.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <sched.h>
 #include <ucontext.h>
 #include <signal.h>
 #include <unistd.h>
@@ -116,8 +120,28 @@ static struct {
 	double seconds;
 	uint32_t n, arena;
 	struct ixg_rx_async_cfg acfg;
+	int pin;
 } opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 0, 0, 2.0, 64, 1u << 16,
-	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}};
+	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}, 0};
+
+/* thread i -> the (pin * i)-th CPU the process may run on; 0 or -errno */
+static int pin_thread(pthread_t th, int i)
+{
+	cpu_set_t all, one;
+	if (sched_getaffinity(0, sizeof(all), &all))
+		return -1;
+	const int n = CPU_COUNT(&all), want = (opt.pin * i) % (n ? n : 1);
+	for (int cpu = 0, k = 0; cpu < CPU_SETSIZE; cpu++) {
+		if (!CPU_ISSET(cpu, &all))
+			continue;
+		if (k++ == want) {
+			CPU_ZERO(&one);
+			CPU_SET(cpu, &one);
+			return -pthread_setaffinity_np(th, sizeof(one), &one);
+		}
+	}
+	return -1;
+}
 
 static const uint8_t rss_key[40] = {0x6d, 0x5a, 0x56, 0xda, 0x25, 0x5b, 0x0e, 0xc2, 0x41, 0x67, 0x25, 0x3d, 0x43, 0xa3,
 				    0x8f, 0xb0, 0xd0, 0xca, 0x2b, 0xcb, 0xae, 0x7b, 0x30, 0xb4, 0x77, 0xcb, 0x2d, 0xa3,
@@ -393,6 +417,8 @@ static int run_loop(void)
 	for (int i = 0; i < opt.threads; i++) {
 		ws[i].t_end = t_start + opt.seconds;
 		pthread_create(&ws[i].th, NULL, work, &ws[i]);
+		if (opt.pin && pin_thread(ws[i].th, i))
+			fprintf(stderr, "pin: thread %d not pinned\n", i);
 	}
 	pthread_barrier_wait(&bar);
 	t_start = now_s();
@@ -473,7 +499,7 @@ static int run_loop(void)
 	       "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"n\": %zu}, "
 	       "\"staged_bytes_per_frame\": %.1f, \"inplace_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
 	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d, "
-	       "\"zero_copy\": %d, \"arena_pages\": \"%s\"}, "
+	       "\"zero_copy\": %d, \"arena_pages\": \"%s\", \"pin\": %d}, "
 	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}, "
 	       "\"breakdown\": {\"thread_ns_per_frame\": %.2f, \"gather_ns_per_frame\": %.2f, \"launch_us_per_batch\": %.2f, "
 	       "\"poll_ns_per_frame\": %.2f, \"wait_ns_per_frame\": %.2f, \"dispatch_ns_per_frame\": %.2f, "
@@ -485,7 +511,7 @@ static int run_loop(void)
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
 	       nl ? lat[nl - 1] : 0.0, nl, staged_b, inplace_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
-	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, arena_pages, (unsigned long long)st.tcp,
+	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, arena_pages, opt.pin, (unsigned long long)st.tcp,
 	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
 	       (unsigned long long)st.drop, el * opt.threads * 1e9 / fr, g_ns / fr,
 	       batches ? l_ns / (double)batches / 1e3 : 0.0, p_ns / fr, w_ns / fr, d_s * 1e9 / fr,
@@ -618,6 +644,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(k, "register")) opt.reg = atoi(v);
 		else if (!strcmp(k, "pages")) opt.small_pages = !strcmp(v, "4k");
 		else if (!strcmp(k, "idle")) opt.spin = !strcmp(v, "spin");
+		else if (!strcmp(k, "pin")) opt.pin = atoi(v);
 		else {
 			fprintf(stderr, "unknown option %s\n", k);
 			return 2;

@@ -22,6 +22,8 @@ box: one JSON line per point, with the run's cgroup CPU throttling
        tailab:L1,L2,..  the 16-thread tail: C2 frames staged and 1514-B frames
                 zero copy, library builds interleaved over 3 rounds, with the
                 worst batch's latency split and the cgroup throttling
+       pin      the 16-thread tail with the threads pinned one per CPU at
+                strides 0 (unpinned) / 8 / 2, C2 staged and 1514-B zero copy
        ab:L1,L2,..  (or L1+L2+..) 16 threads, idle=wait, library builds interleaved over 4
                 rounds (each Li a directory holding a libixgrx.so, or
                 "default"): same-box A/B of host-path library variants
@@ -124,6 +126,14 @@ def main():
                     env = None if lib == "default" else {"LD_LIBRARY_PATH": lib}
                     point(fb, dict(lib=lib, rep=rep, batch_bytes=bb, zero_copy=reg), env=env, threads=16,
                           seconds=sec, arena=1 << 15, register=reg, cfg_bytes=bb)
+    elif which == "pin":
+        fb = os.path.join(tmp, "frames1514.bin")
+        bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
+        for rep in range(3):
+            for pin in (0, 8, 2):
+                point(f, dict(pin=pin, rep=rep, frames=60), threads=16, seconds=sec, arena=1 << 17, pin=pin)
+                point(fb, dict(pin=pin, rep=rep, frames=1514, zero_copy=1), threads=16, seconds=sec,
+                      arena=1 << 15, register=1, pin=pin)
     elif which.startswith("tailab:"):
         fb = os.path.join(tmp, "frames1514.bin")
         bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
