@@ -1976,7 +1976,6 @@ struct FlatLds {
   lds_u32* xch;    // [64 * 4] the chunk's frames {offset lo, hi, L, -} for the copies
   lds_u32* pre[2]; // [64 * kPrefixDw] prefixes, frame-major (DMA), per row set
   lds_u32* ve[2];  // [64 * 4] end pieces (DMA), per row set
-  lds_u32* pf;     // [64] the prefetch's landing slot (never read)
 };
 
 struct FlatPlan {
@@ -2047,19 +2046,6 @@ DEV void flat_dma(const KParams& p, const FlatPlan& f, const GDesc& g, int lane0
   const uint8_t* se = f.nb && g.L > (uint32_t)kStreamBase && (e & 15u) ? p.base + f.A + (e & ~15ull)
                                                                       : p.zero + 16 * lane;
   __builtin_amdgcn_global_load_lds((const void*)se, (__attribute__((address_space(3))) void*)ve, 16, 0, 0);
-}
-
-// The next chunk's span into L2 while this chunk parses: one dword per
-// 128-byte line, copied into a scratch LDS slot (no registers held; the rows
-// issued for that chunk later hit L2 instead of HBM)
-DEV void flat_prefetch(const KParams& p, const FlatPlan& f, int lane, lds_u32* pf) {
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const uint32_t o = 128u * ((uint32_t)lane + 64u * (uint32_t)t);
-    if (o < f.nb)
-      __builtin_amdgcn_global_load_lds((const void*)(p.base + f.A + o), (__attribute__((address_space(3))) void*)pf, 4,
-                                       0, 0);
-  }
 }
 
 // one's complement (end-around carry) sum of a piece's four dwords
@@ -2239,7 +2225,6 @@ DEV void flat_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveL
       flat_blocks(lane, fl);
       __builtin_amdgcn_s_waitcnt(kGldsWait);
       __builtin_amdgcn_wave_barrier();
-      if (j + 1 < nq) flat_prefetch(p, flat_plan(p, q[j + 1], D1, lane), lane, fl.pf);
       uint32_t d[kPrefixDw];
       const lds_u32* row = fl.pre[0] + (uint32_t)lane * kPrefixDw;
       d[0] = d[1] = d[2] = 0;  // MAC addresses: never read
@@ -2325,8 +2310,7 @@ DEV void general_body(const KParams& p) {
   // (FLAT: the span sums; the per-segment path's lists live in them, and
   // the frames' exchange for the staging copies in the end pieces' buffer)
   constexpr int kFw = FLAT ? kWaves : 1;
-  __shared__ uint32_t sh_S[kFw][FLAT ? kFlatS : 1], sh_E[kFw][FLAT ? 64 : 1], sh_ve[kFw][FLAT ? 256 : 1],
-      sh_pf[kFw][FLAT ? 64 : 1];
+  __shared__ uint32_t sh_S[kFw][FLAT ? kFlatS : 1], sh_E[kFw][FLAT ? 64 : 1], sh_ve[kFw][FLAT ? 256 : 1];
   constexpr int kLw = FLAT ? 1 : kWaves;
   __shared__ uint32_t sh_list[kLw][64], sh_end[kLw][64], sh_offlo[kLw][64], sh_offhi[kLw][64], sh_sum[kLw][64],
       sh_q[kWaves][64 * kQGroups];
@@ -2410,8 +2394,7 @@ DEV void general_body(const KParams& p) {
                                FlatLds{LDS(lds_u32, sh_S[FLAT ? wave : 0]), LDS(lds_u32, sh_E[FLAT ? wave : 0]),
                                        LDS(lds_u32, sh_ve[FLAT ? wave : 0]),
                                        {LDS(lds_u32, sh_pre[wave]), LDS(lds_u32, sh_pre[wave])},
-                                       {LDS(lds_u32, sh_ve[FLAT ? wave : 0]), LDS(lds_u32, sh_ve[FLAT ? wave : 0])},
-                                       LDS(lds_u32, sh_pf[FLAT ? wave : 0])},
+                                       {LDS(lds_u32, sh_ve[FLAT ? wave : 0]), LDS(lds_u32, sh_ve[FLAT ? wave : 0])}},
                                q, nq, lane, D0);
     else if (!SEARLY || wave_any(D0.L > (uint32_t)kStreamBase + 32u))
       gen_walk<OFFS, false, kModeLong, SM, LATE, BIGOK, DMX>(p, T, w, q, nq, lane, D0);
