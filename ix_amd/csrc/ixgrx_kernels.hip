@@ -2235,7 +2235,9 @@ DEV void flat_walk(const KParams& p, const uint64_t* __restrict__ T, const WaveL
         d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
       }
       const u32x4 ve = *(const lds_u32x4*)(fl.ve[0] + 4u * (uint32_t)lane);
-      mask_prefix(d, D0.L);
+      // (no mask_prefix: the copies zero-fill the pieces at or past L and the
+      // parse masks the two fields it can read past L; C3 -0.8 %, VALU per
+      // chunk 1038 -> 873, profiles/r06/flat/ab_c3_nomask*.json)
       if (wave_all(c * 64u + (uint32_t)lane >= p.n || (eth_type(d, D0.L) == 0x0800u && byte_at(d, 14) == 0x45u)))
         flat_finish<kShapeFixed, DMX>(p, T, c, lane, w, fl, F, D0, d, ve);
       else
