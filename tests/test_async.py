@@ -409,3 +409,4 @@ def test_worst_batch_split(direct):
     assert st["worst_total_ns"] > 0 and parts == st["worst_total_ns"], st
     assert st["worst_gpu_ns"] > 0, st          # the device clock was read and calibrated
     assert st["worst_wait_ns"] <= st["worst_total_ns"]
+    assert st["worst_nap_max_ns"] <= st["worst_wait_ns"] and (st["worst_naps"] == 0) == (st["worst_nap_max_ns"] == 0)

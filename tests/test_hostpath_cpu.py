@@ -450,6 +450,9 @@ def test_async_stats_counters(fake):
         assert st["worst_total_ns"] > 0 and st["worst_gpu_ns"] == 0
         assert st["worst_open_ns"] + st["worst_visible_ns"] + st["worst_returned_ns"] == st["worst_total_ns"]
         assert st["worst_wait_ns"] <= st["worst_total_ns"]
+        # poll(wait)'s naps: the worst batch's longest nap is part of its wait
+        assert st["worst_nap_max_ns"] <= st["worst_wait_ns"] and st["nap_max_ns"] <= st["wait_ns"]
+        assert (st["worst_naps"] == 0) == (st["worst_nap_max_ns"] == 0)
         assert eng.async_stats()["frames_submitted"] == 0   # reset
         assert eng.async_stats()["worst_total_ns"] == 0
     finally:
