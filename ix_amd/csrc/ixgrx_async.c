@@ -80,7 +80,6 @@ struct ixg_async {
 	/* the device's wall clock -> CLOCK_MONOTONIC ns: ns = ticks * gclk_mul + gclk_off
 	 * (gclk_mul 0: unknown) */
 	double gclk_mul, gclk_off;
-	uint64_t lat_avg;    /* ns: a batch's launch -> done on the device (moving average; 0: none yet) */
 	struct ixg_abatch b[IXG_ASYNC_MAX_DEPTH];
 };
 
@@ -234,7 +233,7 @@ static void batch_returned(struct ixg_async *a, const struct ixg_abatch *b, uint
 
 /* the library saw batch b's completion word (its stamp's device clock: when
  * the stamp ran, in CLOCK_MONOTONIC ns; 0 when unknown) */
-static void batch_seen(struct ixg_async *a, struct ixg_abatch *b)
+static void batch_seen(const struct ixg_async *a, struct ixg_abatch *b)
 {
 	b->t_seen = now_ns();
 	b->t_gpu = 0;
@@ -243,11 +242,6 @@ static void batch_seen(struct ixg_async *a, struct ixg_abatch *b)
 		const double t = (double)g * a->gclk_mul + a->gclk_off;
 		b->t_gpu = t > 0 ? (uint64_t)t : 0;
 	}
-	/* the device time of a batch (the stamp's clock when known: a late look
-	 * at the word says nothing about the device), for poll(wait)'s first nap */
-	const uint64_t d = b->t_gpu > b->t_launch && b->t_gpu <= b->t_seen ? b->t_gpu - b->t_launch
-	                                                                  : b->t_seen - b->t_launch;
-	a->lat_avg = a->lat_avg ? a->lat_avg - a->lat_avg / 8 + d / 8 : d;
 }
 
 int ixg_rx_async_init(void *vctx, const struct ixg_rx_async_cfg *cfg)
@@ -561,17 +555,7 @@ static int wait_word(struct ixg_ctx *c, struct ixg_abatch *b, uint64_t t0, struc
 				sv->changed = 1;
 			}
 		}
-		/* The first nap sleeps through most of the batch's expected device
-		 * time (3/4 of the moving average, at most 1 ms), the later ones 10 us:
-		 * fewer wake-ups, and each is a chance for the host's scheduler to
-		 * return the thread late */
-		long ns = IXG_WAIT_NAP_NS;
-		if (!b->naps && c->async->lat_avg) {
-			const uint64_t want = c->async->lat_avg * 3 / 4, el = now_ns() - b->t_launch;
-			if (want > el + 2 * IXG_WAIT_NAP_NS)
-				ns = (long)(want - el < 1000000ull ? want - el : 1000000ull);
-		}
-		const struct timespec nap = {0, ns};
+		const struct timespec nap = {0, IXG_WAIT_NAP_NS};
 		const uint64_t n0 = now_ns();
 		nanosleep(&nap, NULL);
 		const uint64_t dn = now_ns() - n0;
