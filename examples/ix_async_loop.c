@@ -36,6 +36,10 @@
  *   pin=K: thread i runs on the K*i-th CPU of the process's allowed set (as
  *   IX pins one thread per dedicated core, dp/core/cpu.c); 0 (the default):
  *   the scheduler places the threads
+ *   pinset=K: thread i may run on the K CPUs from the K*i-th of the lower
+ *   half of the allowed set and on their SMT siblings in the upper half
+ *   (K = 8 on the GPU box: one core complex, its L3, per thread), and the
+ *   scheduler picks among them
  * FRAMES_FILE: u32 count, u16 lengths[count], then the frames back to back.
  * dump=FILE (loop mode): thread 0's first `count` records, in submission
  * order, for the caller's parity check against the oracle.
@@ -120,16 +124,32 @@ static struct {
 	double seconds;
 	uint32_t n, arena;
 	struct ixg_rx_async_cfg acfg;
-	int pin;
+	int pin, pinset;
 } opt = {NULL, "loop", NULL, 1, 64, 0, 0, 0, 0, 0, 2.0, 64, 1u << 16,
-	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}, 0};
+	 {IXG_ASYNC_DEF_FRAMES, IXG_ASYNC_DEF_BYTES, IXG_ASYNC_DEF_WAIT_US, IXG_ASYNC_DEF_DEPTH, IXG_ASYNC_DEF_FLAGS}, 0, 0};
 
-/* thread i -> the (pin * i)-th CPU the process may run on; 0 or -errno */
+/* thread i -> the (pin * i)-th CPU the process may run on, or (pinset) the
+ * (pinset * i)-th block of pinset CPUs of the allowed set's lower half with
+ * their upper-half siblings; 0 or -errno */
 static int pin_thread(pthread_t th, int i)
 {
 	cpu_set_t all, one;
 	if (sched_getaffinity(0, sizeof(all), &all))
 		return -1;
+	if (opt.pinset) {
+		int list[CPU_SETSIZE], n = 0;
+		for (int cpu = 0; cpu < CPU_SETSIZE; cpu++)
+			if (CPU_ISSET(cpu, &all))
+				list[n++] = cpu;
+		const int half = n / 2 ? n / 2 : 1, b = (opt.pinset * i) % half;
+		CPU_ZERO(&one);
+		for (int k = 0; k < opt.pinset && b + k < half; k++) {
+			CPU_SET(list[b + k], &one);
+			if (half + b + k < n)
+				CPU_SET(list[half + b + k], &one);
+		}
+		return -pthread_setaffinity_np(th, sizeof(one), &one);
+	}
 	const int n = CPU_COUNT(&all), want = (opt.pin * i) % (n ? n : 1);
 	for (int cpu = 0, k = 0; cpu < CPU_SETSIZE; cpu++) {
 		if (!CPU_ISSET(cpu, &all))
@@ -417,7 +437,7 @@ static int run_loop(void)
 	for (int i = 0; i < opt.threads; i++) {
 		ws[i].t_end = t_start + opt.seconds;
 		pthread_create(&ws[i].th, NULL, work, &ws[i]);
-		if (opt.pin && pin_thread(ws[i].th, i))
+		if ((opt.pin || opt.pinset) && pin_thread(ws[i].th, i))
 			fprintf(stderr, "pin: thread %d not pinned\n", i);
 	}
 	pthread_barrier_wait(&bar);
@@ -499,7 +519,7 @@ static int run_loop(void)
 	       "\"latency_us\": {\"p50\": %.1f, \"p99\": %.1f, \"max\": %.1f, \"n\": %zu}, "
 	       "\"staged_bytes_per_frame\": %.1f, \"inplace_bytes_per_frame\": %.1f, \"record_bytes_per_frame\": 16, "
 	       "\"cfg\": {\"batch_frames\": %u, \"batch_bytes\": %u, \"max_wait_us\": %u, \"depth\": %u, \"direct\": %d, "
-	       "\"zero_copy\": %d, \"arena_pages\": \"%s\", \"pin\": %d}, "
+	       "\"zero_copy\": %d, \"arena_pages\": \"%s\", \"pin\": %d, \"pinset\": %d}, "
 	       "\"verdicts\": {\"tcp\": %llu, \"udp\": %llu, \"icmp\": %llu, \"arp\": %llu, \"drop\": %llu}, "
 	       "\"breakdown\": {\"thread_ns_per_frame\": %.2f, \"gather_ns_per_frame\": %.2f, \"launch_us_per_batch\": %.2f, "
 	       "\"poll_ns_per_frame\": %.2f, \"wait_ns_per_frame\": %.2f, \"dispatch_ns_per_frame\": %.2f, "
@@ -511,7 +531,7 @@ static int run_loop(void)
 	       opt.threads, el, (unsigned long long)frames, frames / el / 1e6, (unsigned long long)iters,
 	       iters ? (double)frames / (double)iters : 0.0, opt.batch, pct(lat, nl, 0.5), pct(lat, nl, 0.99),
 	       nl ? lat[nl - 1] : 0.0, nl, staged_b, inplace_b, opt.acfg.batch_frames, opt.acfg.batch_bytes, opt.acfg.max_wait_us,
-	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, arena_pages, opt.pin, (unsigned long long)st.tcp,
+	       opt.acfg.depth, (opt.acfg.flags & IXG_ASYNC_DIRECT) ? 1 : 0, opt.reg, arena_pages, opt.pin, opt.pinset, (unsigned long long)st.tcp,
 	       (unsigned long long)st.udp, (unsigned long long)st.icmp, (unsigned long long)st.arp,
 	       (unsigned long long)st.drop, el * opt.threads * 1e9 / fr, g_ns / fr,
 	       batches ? l_ns / (double)batches / 1e3 : 0.0, p_ns / fr, w_ns / fr, d_s * 1e9 / fr,
@@ -645,6 +665,7 @@ int main(int argc, char **argv)
 		else if (!strcmp(k, "pages")) opt.small_pages = !strcmp(v, "4k");
 		else if (!strcmp(k, "idle")) opt.spin = !strcmp(v, "spin");
 		else if (!strcmp(k, "pin")) opt.pin = atoi(v);
+		else if (!strcmp(k, "pinset")) opt.pinset = atoi(v);
 		else {
 			fprintf(stderr, "unknown option %s\n", k);
 			return 2;

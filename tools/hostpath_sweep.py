@@ -126,14 +126,17 @@ def main():
                     env = None if lib == "default" else {"LD_LIBRARY_PATH": lib}
                     point(fb, dict(lib=lib, rep=rep, batch_bytes=bb, zero_copy=reg), env=env, threads=16,
                           seconds=sec, arena=1 << 15, register=reg, cfg_bytes=bb)
-    elif which == "pin":
+    elif which == "pin" or which.startswith("pin:"):
+        PINS = which[4:].split(",") if which.startswith("pin:") else ("0", "8", "2")
         fb = os.path.join(tmp, "frames1514.bin")
         bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
         for rep in range(3):
-            for pin in (0, 8, 2):
-                point(f, dict(pin=pin, rep=rep, frames=60), threads=16, seconds=sec, arena=1 << 17, pin=pin)
+            for pin in PINS:
+                # "sK": pinset=K (a block of K CPUs and their SMT siblings per thread)
+                kw = dict(pinset=int(pin[1:])) if str(pin).startswith("s") else dict(pin=int(pin))
+                point(f, dict(pin=pin, rep=rep, frames=60), threads=16, seconds=sec, arena=1 << 17, **kw)
                 point(fb, dict(pin=pin, rep=rep, frames=1514, zero_copy=1), threads=16, seconds=sec,
-                      arena=1 << 15, register=1, pin=pin)
+                      arena=1 << 15, register=1, **kw)
     elif which.startswith("tailab:"):
         fb = os.path.join(tmp, "frames1514.bin")
         bench.write_frames_file(traces.make_trace("tcp1514", 1 << 14, seed=0x1BF001), fb)
