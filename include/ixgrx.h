@@ -458,6 +458,15 @@ int ixg_rx_tcpx_batch_dev(void *ctx, const struct ixg_rx_frames *frames, uint32_
 int ixg_icmp_reflect_dev(void *ctx, const struct ixg_rx_frames *frames, const struct ixg_rx_rec *d_rec, uint32_t n,
 			 const uint8_t mac[6], uint32_t host_addr, void *stream);
 
+/* ixg_rx_batch_dev and then ixg_icmp_reflect_dev in one call: the records
+ * of the frames, and every IXG_V_ICMP_ECHO frame rewritten in place into its
+ * echo reply as above, its record carrying IXG_RF_REPLY (eth_input ->
+ * icmp_input -> icmp_reflect per echo request, dp/net/ip.c:120-141,
+ * dp/net/icmp.c:44-71,88-92). Arguments as ixg_rx_batch_dev plus the
+ * reply's mac / host_addr. Asynchronous on `stream`. 0 or -errno. */
+int ixg_rx_icmp_batch_dev(void *ctx, const struct ixg_rx_frames *frames, uint32_t n, struct ixg_rx_rec *d_out,
+			  const uint8_t mac[6], uint32_t host_addr, void *stream);
+
 /* ---- PCB demux: the tcp_input step after the head ---- */
 
 /* For each IXG_V_TCP record, find the PCB the segment belongs to, exactly as

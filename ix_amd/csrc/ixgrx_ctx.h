@@ -157,10 +157,15 @@ IXG_INTERNAL int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const u
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t lflags, hipStream_t s);
 /* ixg_launch_ds with the tcp_input head (ext != NULL: ixg_rx_tcpx_batch_dev) */
+/* the echo replies of ixg_rx_icmp_batch_dev (CFG.mac, CFG.host_addr in host order) */
+struct ixg_icmp_fuse {
+	uint8_t mac[6];
+	uint32_t host_addr;
+};
 IXG_INTERNAL int ixg_launch_x(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 			      const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 			      struct ixg_demux_rec *dmx, struct ixg_tcp_ext *ext, uint32_t xflags, uint32_t lflags,
-			      hipStream_t s);
+			      const struct ixg_icmp_fuse *ic, hipStream_t s);
 IXG_INTERNAL void ixg_dstate_free(struct ixg_dstate *ds);
 /* the per-chunk defer flags for batches of up to nchunks chunks (grown, never
  * shrunk; growing frees the old buffer, which waits for the device) */

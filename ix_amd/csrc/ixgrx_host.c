@@ -264,12 +264,13 @@ int ixg_launch_ds(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base,
 		  const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
 		  struct ixg_demux_rec *dmx, uint32_t overlap, hipStream_t s)
 {
-	return ixg_launch_x(c, ds, base, off, len, stride, n, out, csum, dmx, NULL, 0, overlap, s);
+	return ixg_launch_x(c, ds, base, off, len, stride, n, out, csum, dmx, NULL, 0, overlap, NULL, s);
 }
 
 int ixg_launch_x(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, const uint64_t *off,
 		 const uint16_t *len, uint32_t stride, uint32_t n, struct ixg_rx_rec *out, uint32_t *csum,
-		 struct ixg_demux_rec *dmx, struct ixg_tcp_ext *ext, uint32_t xflags, uint32_t overlap, hipStream_t s)
+		 struct ixg_demux_rec *dmx, struct ixg_tcp_ext *ext, uint32_t xflags, uint32_t overlap,
+		 const struct ixg_icmp_fuse *ic, hipStream_t s)
 {
 	struct ixg_kparams p;
 	memset(&p, 0, sizeof(p));
@@ -316,6 +317,25 @@ int ixg_launch_x(struct ixg_ctx *c, struct ixg_dstate *ds, const uint8_t *base, 
 			ds->epoch = 1;
 		p.epoch = ds->epoch;
 		p.force_mode = c->force_mode;
+	}
+	if (ic) {
+		/* the echo replies: the reflect pass behind the RX kernels, marking
+		 * the records it answers (replies built in the span-staged kernel
+		 * from its registers measured slower: DESIGN.md 8, round 6) */
+		if (ixgrx_launch(&p, c->ncu, s) != 0)
+			return -EIO;
+		struct ixg_iparams ip;
+		memset(&ip, 0, sizeof(ip));
+		ip.base = (uint8_t *)(uintptr_t)base;
+		ip.off = off;
+		ip.rec = out;
+		ip.stride = stride;
+		ip.n = n;
+		memcpy(ip.mac, ic->mac, 6);
+		const uint32_t be = __builtin_bswap32(ic->host_addr); /* hton32 (icmp.c:55) */
+		memcpy(ip.host, &be, 4);
+		ip.mark = 1;
+		return ixgrx_icmp_launch(&ip, s) == 0 ? 0 : -EIO;
 	}
 	if (!ext)
 		return ixgrx_launch(&p, c->ncu, s) == 0 ? 0 : -EIO;
@@ -1162,7 +1182,27 @@ int ixg_rx_tcpx_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n
 	if (hipSetDevice(c->device) != hipSuccess)
 		return -EIO;
 	return ixg_launch_x(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, NULL,
-			    d_ext, flags, 0, (hipStream_t)stream);
+			    d_ext, flags, 0, NULL, (hipStream_t)stream);
+}
+
+int ixg_rx_icmp_batch_dev(void *vctx, const struct ixg_rx_frames *fr, uint32_t n, struct ixg_rx_rec *d_out,
+			  const uint8_t mac[6], uint32_t host_addr, void *stream)
+{
+	struct ixg_ctx *c = (struct ixg_ctx *)vctx;
+	if (!c || !fr || !mac || (n && (!fr->base || !fr->len || !d_out)))
+		return -EINVAL;
+	if (n == 0)
+		return 0;
+	if (((uintptr_t)fr->base & 3) || (!fr->off && (fr->stride & 3)) || ((uintptr_t)d_out & 15) ||
+	    ((uintptr_t)fr->len & 1) || ((uintptr_t)fr->off & 7))
+		return -EINVAL;
+	if (hipSetDevice(c->device) != hipSuccess)
+		return -EIO;
+	struct ixg_icmp_fuse ic;
+	memcpy(ic.mac, mac, 6);
+	ic.host_addr = host_addr;
+	return ixg_launch_x(c, &c->ds, (const uint8_t *)fr->base, fr->off, fr->len, fr->stride, n, d_out, NULL, NULL,
+			    NULL, 0, 0, &ic, (hipStream_t)stream);
 }
 
 int ixg_tcp_ext_batch_dev(void *vctx, const struct ixg_rx_frames *fr, const struct ixg_rx_rec *d_rec, uint32_t n,

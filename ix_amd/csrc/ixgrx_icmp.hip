@@ -206,6 +206,7 @@ DEV bool flood_wave(const ixg_iparams& p, uint64_t i, int lane, bool valid, bool
     f[moff] = 0u;
     f[moff + 2u] = (uint8_t)(ck & 0xffu);
     f[moff + 3u] = (uint8_t)(ck >> 8);
+    mark_reply(p, i);  // (no item list on this path: item i is record i)
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();

@@ -14,7 +14,7 @@ import ctypes
 
 from ix_amd import ixgrx
 
-EXPORTS = ("ixg_icmp_reflect_dev",)
+EXPORTS = ("ixg_icmp_reflect_dev", "ixg_rx_icmp_batch_dev")
 
 
 def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
@@ -23,6 +23,8 @@ def _bind(lib: ctypes.CDLL) -> ctypes.CDLL:
     vp, u32, i32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     lib.ixg_icmp_reflect_dev.argtypes = [vp, ctypes.POINTER(ixgrx.RxFrames), vp, u32, vp, u32, vp]
     lib.ixg_icmp_reflect_dev.restype = i32
+    lib.ixg_rx_icmp_batch_dev.argtypes = [vp, ctypes.POINTER(ixgrx.RxFrames), u32, vp, vp, u32, vp]
+    lib.ixg_rx_icmp_batch_dev.restype = i32
     lib._ixg_icmp_bound = True
     return lib
 
@@ -39,3 +41,17 @@ def reflect_dev(eng: ixgrx.RxEngine, base: int, off: int | None, stride: int, re
     m = (ctypes.c_uint8 * 6).from_buffer_copy(bytes(mac))
     ixgrx._check(lib.ixg_icmp_reflect_dev(eng._ctx, ctypes.byref(fr), rec, n, m, host_addr, stream or None),
                  "ixg_icmp_reflect_dev", lib)
+
+
+def rx_batch_dev(eng: ixgrx.RxEngine, base: int, off: int | None, lens: int, stride: int, n: int, rec: int,
+                 mac: bytes, host_addr: int, stream: int | None = None) -> None:
+    """ixg_rx_icmp_batch_dev: the records (rec, n x 16 B) and the echo
+    replies in place in one launch. Device pointers as ints; asynchronous on
+    `stream`."""
+    lib = _bind(eng._lib)
+    if len(mac) != 6:
+        raise ValueError("mac: 6 bytes")
+    fr = ixgrx.RxFrames(base, off or None, lens, stride, 0)
+    m = (ctypes.c_uint8 * 6).from_buffer_copy(bytes(mac))
+    ixgrx._check(lib.ixg_rx_icmp_batch_dev(eng._ctx, ctypes.byref(fr), n, rec, m, host_addr, stream or None),
+                 "ixg_rx_icmp_batch_dev", lib)

@@ -53,7 +53,7 @@ EXPORTS = (
     "ixg_rx_async_init", "ixg_rx_submit_mbufs", "ixg_rx_flush", "ixg_rx_poll", "ixg_rx_async_pending",
     "ixg_rx_async_stats",
     "ixg_rx_register_memory", "ixg_rx_unregister_memory", "ixg_tcp_ext_batch_dev", "ixg_rx_tcpx_batch_dev",
-    "ixg_icmp_reflect_dev",
+    "ixg_icmp_reflect_dev", "ixg_rx_icmp_batch_dev",
     "ixg_rx_set_icmp_reply",
 )
 

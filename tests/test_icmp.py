@@ -311,3 +311,105 @@ def test_gpu_flood_span_path(layout):
         eng.close()
     bad = np.nonzero(out != exp)[0]
     assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+
+
+# ---- ixg_rx_icmp_batch_dev: RX records and the replies in one call -------------
+
+def _dev_rx_icmp(eng, tr, mac, host):
+    import torch
+    dev = torch.device("cuda", 0)
+    n = tr.n
+    b = torch.from_numpy(np.concatenate([np.ascontiguousarray(tr.blob, dtype=np.uint8),
+                                         np.zeros(ixgrx.IXG_TAIL_PAD, np.uint8)])).to(dev)
+    o = None if tr.off is None or tr.stride else \
+        torch.from_numpy(np.ascontiguousarray(tr.off, dtype=np.uint64).view(np.int64)).to(dev)
+    ln = torch.from_numpy(np.ascontiguousarray(tr.len, dtype=np.uint16).view(np.int16)).to(dev)
+    rec = torch.full((n, 16), 0x5A, dtype=torch.uint8, device=dev)
+    icmp.rx_batch_dev(eng, b.data_ptr(), None if o is None else o.data_ptr(), ln.data_ptr(), tr.stride or 0, n,
+                      rec.data_ptr(), mac, host)
+    torch.cuda.synchronize()
+    return rec.cpu().numpy(), b.cpu().numpy()[:tr.blob.size]
+
+
+def _fused_expect(tr, key, mac, host):
+    er, _ = oracle.rx_trace(tr, key)
+    exp, k = oracle.icmp_reflect_batch(tr.blob, tr.off, tr.stride or 0, er, mac, host)
+    er = er.copy()
+    echo = er[:, 2] == ixgrx.V["ICMP_ECHO"]
+    er[echo, 3] |= 0x40  # IXG_RF_REPLY
+    return er, exp, int(k)
+
+
+def _check_fused(tr, key, mac, host):
+    er, exp, k = _fused_expect(tr, key, mac, host)
+    eng = ixgrx.RxEngine(ixgrx.Config(key))
+    try:
+        rec, out = _dev_rx_icmp(eng, tr, mac, host)
+    finally:
+        eng.close()
+    badr = np.nonzero((rec != er).any(axis=1))[0]
+    assert badr.size == 0, f"{badr.size} records differ, first {badr[:6].tolist()}: {rec[badr[0]].tolist()} vs " \
+                           f"{er[badr[0]].tolist()}"
+    bad = np.nonzero(out != exp)[0]
+    assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    return k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("which", ["", "2"])
+def test_gpu_rx_icmp_golden(golden, which):
+    """The reference's frames (echo requests among every other ICMP and
+    non-ICMP case of the fixture) through ixg_rx_icmp_batch_dev: records as
+    the reference's with IXG_RF_REPLY on the echo requests, frames as the
+    reference's icmp_input left them."""
+    g = golden
+    off = g["off"].astype(np.uint64)
+    frames = [g["blob"][int(o):int(o) + int(L)].tobytes() for o, L in zip(off, g["len"])]
+    tr = traces.pack(frames)  # 4-aligned starts (the ABI's requirement)
+    k = _check_fused(tr, bytes(g["key"]), bytes(g["mac"]), int(g["host_addr" + which]))
+    assert k == int(g["reflected"].sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("layout", ["offsets", "stride"])
+def test_gpu_rx_icmp_mixed_vs_oracle(layout):
+    """Default-size pings, long pings, pings with IP options, pings with bad
+    checksums, TCP frames, and chunks of 1514-B frames (the long kernel's,
+    with pings among them): records (IXG_RF_REPLY on every answered request)
+    and every byte against the oracle."""
+    rng = np.random.default_rng(0x1C9 + (layout == "stride"))
+    frames = []
+    for c in range(300):
+        big = c % 10 == 3 and layout == "offsets"
+        for _ in range(64):
+            u = rng.random()
+            if big and u < 0.5:
+                frames.append(bytes(traces.build_ipv4(rng, 1, 1514, 6)[0]))
+            elif u < 0.55:
+                frames.append(traces.icmp_echo(rng, int(rng.integers(0, 55 if layout == "stride" else 71))))
+            elif u < 0.65:
+                frames.append(traces.icmp_echo(rng, int(rng.integers(40, 55)) if layout == "stride"
+                                               else int(rng.integers(71, 1400))))
+            elif u < 0.72:
+                frames.append(traces.icmp_echo(rng, int(rng.integers(0, 60)), ihl=6))
+            elif u < 0.8:
+                f = bytearray(traces.icmp_echo(rng, int(rng.integers(0, 60))))
+                f[int(rng.integers(34, len(f)))] ^= 0x10
+                frames.append(bytes(f))
+            else:
+                frames.append(bytes(traces.build_ipv4(rng, 1, 60, 6)[0]))
+    # (stride 96: chunks span-staged, as packed ones)
+    tr = traces.pack(frames, stride=96) if layout == "stride" else traces.pack(frames)
+    k = _check_fused(tr, traces.RSS_KEY, bytes([2, 3, 5, 7, 11, 13]), 0x0a0b0c0d)
+    assert k > len(frames) // 3
+
+
+@pytest.mark.gpu
+def test_gpu_rx_icmp_ping_flood():
+    """A flood of default pings (the reflect pass's span path, which marks
+    its records too) and a ragged batch end."""
+    rng = np.random.default_rng(0x1CB)
+    pool = [traces.icmp_echo(rng, 56) for _ in range(512)]
+    tr = traces.pack(pool * 256 + pool[:77])
+    k = _check_fused(tr, traces.RSS_KEY, bytes([2, 9, 8, 7, 6, 5]), 0xc0a80001)
+    assert k == tr.n
