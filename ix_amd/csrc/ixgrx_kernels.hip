@@ -1960,7 +1960,7 @@ ixg_rx_fastc_tcpx_s(KParams p) {
 // The rows (120 VGPRs) are live only while no parse state is: 256 VGPRs, two
 // waves per SIMD, 8-wave blocks whose span buffers fill the CU's LDS.
 // A chunk that is not flat (span over kFlatRows KiB, frames out of order)
-// takes flat_fallback (per-lane prefixes and tails, 8 pieces in flight).
+// takes flat_fallback (per-lane prefixes and tails, 16 pieces in flight).
 constexpr uint32_t kFlatRows = 30;                 // the largest span taken: 30 KiB (rows + parse in 256 VGPRs)
 constexpr uint32_t kFlatPieces = 64u * kFlatRows;  // its 16-byte pieces
 // S[] holds piece q at q + q / 32: the lane-blocked scan (lane t: pieces
@@ -2155,16 +2155,17 @@ DEV void flat_finish(const KParams& p, const uint64_t* __restrict__ T, uint32_t 
 // A chunk the flat walk does not take (its span over kFlatRows KiB, or its
 // frames out of order; rare in packed batches of IX frames): per-lane
 // prefix loads, the general parse, and each tail [96, seg_end) summed by its
-// own lane, 8 pieces in flight (slow_chunk's path with the loads batched).
+// own lane, 16 pieces in flight (slow_chunk's path with the loads batched;
+// 16 against 8: C3 -1.1 %, profiles/r06/flat/ab_c3_tail16.json).
 // Registers stay within the flat path's own (no streaming rounds).
-DEV uint32_t tail_sum8(const KParams& p, uint64_t off, uint32_t a, uint32_t e) {
+DEV uint32_t tail_sum16(const KParams& p, uint64_t off, uint32_t a, uint32_t e) {
   uint32_t s = 0;
-  for (uint32_t pos = a; wave_any(pos < e); pos += 128u) {
-    u32x4 v[8];
+  for (uint32_t pos = a; wave_any(pos < e); pos += 256u) {
+    u32x4 v[16];
 #pragma unroll
-    for (int k = 0; k < 8; k++) v[k] = load16(pos + 16u * k < e, p.base + off + pos + 16u * k, p.zero);
+    for (int k = 0; k < 16; k++) v[k] = load16(pos + 16u * k < e, p.base + off + pos + 16u * k, p.zero);
 #pragma unroll
-    for (int k = 0; k < 8; k++) s = add1c(s, sum4(mask_piece(v[k], (int)e - (int)(pos + 16u * k))));
+    for (int k = 0; k < 16; k++) s = add1c(s, sum4(mask_piece(v[k], (int)e - (int)(pos + 16u * k))));
   }
   return s;
 }
@@ -2185,7 +2186,7 @@ DEV void flat_fallback(const KParams& p, const uint64_t* __restrict__ T, const W
   uint32_t res = l4_residual(s);
   const bool strm = valid && s.stream;
   if (wave_any(strm)) {
-    const uint32_t t = tail_sum8(p, g.off, (uint32_t)kStreamBase, strm ? s.seg_end : 0u);
+    const uint32_t t = tail_sum16(p, g.off, (uint32_t)kStreamBase, strm ? s.seg_end : 0u);
     if (strm) res = (~fold16(add1c(fold32(s.l4_acc), t))) & 0xffffu;
   }
   if (!valid) return;
