@@ -1918,8 +1918,10 @@ ixg_rx_fastc_s(KParams p) {
   fastc_loop<false>(p, T, LDS(lds_u32, buf[threadIdx.x >> 6]));
 }
 
-// with the fused PCB demux (p.dmx set: ixg_rx_demux_batch_dev)
-extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+// with the fused PCB demux (p.dmx set: ixg_rx_demux_batch_dev); 3 waves per
+// SIMD (168 VGPRs) rather than 4: the lookup's state one chunk behind gets
+// registers, fused demux 0.2948 -> 0.2909 ms (profiles/r06/demux/ab_waves.json)
+extern "C" __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3)))
 ixg_rx_fastc_dmx_s(KParams p) {
   __shared__ uint64_t T[12 * 256];
   __shared__ uint32_t buf[kWaves][1024];
